@@ -1,0 +1,192 @@
+/*
+ * shockwave_amd.h — C-ABI of the MI355X-native Shockwave plan solver.
+ *
+ * Drop-in boundary.  The reference has no FFI: its boundary is the Python
+ * method ShockwaveScheduler.current_round_schedule()
+ * (reference scheduler/shockwave.py:77-91), which builds P1
+ * (_eisenberg_gale_program, shockwave.py:330-388) and P2
+ * (_prioritize_unfair_jobs, shockwave.py:281-328) in CVXPY and hands both to
+ * Gurobi (_solve_gurobi, shockwave.py:400-411).  The native crossing in the
+ * reference is problem.solve() (shockwave.py:401-408).  This header replaces
+ * exactly that crossing: the host mirror (shockwave-replication_amd/shockwave.py)
+ * runs the estimators as the reference does (shockwave.py:111-134, :255-278),
+ * packs the per-job numbers into the SoA arrays below, and calls
+ * sw_plan_solve() in place of the two problem.solve() calls.  The result is the
+ * 0/1 plan that _generate_schedule (shockwave.py:390-398) reads back.
+ *
+ * Conventions
+ *   - Plain C types only.  No C++ exceptions cross this boundary.
+ *   - Caller owns every array passed in or out; the library copies what it
+ *     needs.  The library owns its device buffers (one set per handle).
+ *   - A handle is not thread-safe; the reference calls the solve under
+ *     _scheduler_lock (scheduler.py:1729), so one handle per thread suffices.
+ *   - Return codes: SW_OK (0) = solved; SW_FALLBACK (1) = solved, but P2
+ *     could not place every P1 round and the P1 placement was kept (the
+ *     reference's "P2 has no solution → return P1 schedule", shockwave.py:
+ *     325-326); negative = error, message in sw_last_error().
+ */
+#ifndef SHOCKWAVE_AMD_H
+#define SHOCKWAVE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SW_ABI_VERSION 1
+
+/* Limits of this build. */
+#define SW_MAX_ROUNDS 64 /* future_rounds T (reference configs use 20 and 30) */
+#define SW_MAX_BASES 8   /* len(log_approximation_bases) (reference: 6)        */
+
+/* Return / status codes. */
+#define SW_OK 0
+#define SW_FALLBACK 1          /* P2 failed to place all rounds; P1 plan kept   */
+#define SW_ERR_INVALID (-1)    /* bad sizes or non-finite / out-of-range input */
+#define SW_ERR_HIP (-2)        /* HIP runtime error                             */
+#define SW_ERR_CAPACITY (-3)   /* problem exceeds the handle's reserved sizes  */
+#define SW_ERR_RCCL (-4)       /* RCCL error (sharded mode)                     */
+#define SW_ERR_NOT_BUILT (-5)  /* feature not compiled into this library        */
+
+/* Result status bits (sw_result.status). */
+#define SW_STATUS_P1_REPACKED 0x1 /* aggregate P1 counts needed repair to pack */
+#define SW_STATUS_P2_FALLBACK 0x2 /* P2 placement fell back to the P1 plan    */
+#define SW_STATUS_NO_PLANNED 0x4  /* no job has planned rounds (shockwave.py:319-320) */
+
+/*
+ * One plan solve.  Field ↔ reference:
+ *   num_jobs        len(self.job_metadata)                     shockwave.py:27-28
+ *   future_rounds   self.future_rounds (T)                     shockwave.py:17
+ *   num_gpus        self.num_gpus (G)                          shockwave.py:15
+ *   round_duration  self.round_duration (Δ)                    shockwave.py:16
+ *   regularizer     self.regularizer (k)                       shockwave.py:19
+ *   bases           config["log_approximation_bases"] (β)      shockwave.py:100
+ *   log_bases       log(β_b), log(0) → log(1e-6)               shockwave.py:101-105
+ *   nworkers        job.nworkers (w_j)                         shockwave.py:66
+ *   epoch_duration  np.mean(epoch_durations[:F+1]) (d_j)       shockwave.py:118-120
+ *   completed_epochs job.completed_epochs (F_j)                shockwave.py:133
+ *   total_epochs    job.total_epochs (E_j)                     shockwave.py:134
+ *   remaining_runtime compute_remaining_runtime() call #2 (R_j) shockwave.py:261
+ *   priority        FTF_j ** lambda (p_j)                      shockwave.py:368
+ * All per-job arrays have num_jobs entries, in job_metadata insertion order.
+ */
+typedef struct sw_problem {
+    int32_t num_jobs;
+    int32_t future_rounds;
+    int32_t num_gpus;
+    int32_t num_bases;
+    double round_duration;
+    double regularizer;
+    const double* bases;
+    const double* log_bases;
+    const int32_t* nworkers;
+    const double* epoch_duration;
+    const int32_t* completed_epochs;
+    const int32_t* total_epochs;
+    const double* remaining_runtime;
+    const double* priority;
+} sw_problem;
+
+/*
+ * Outputs.  plan is row-major [num_jobs][future_rounds], 1 = job j runs in
+ * future round t (the round_schedule_vars[j][t] that _generate_schedule reads,
+ * shockwave.py:394-396).  planned_rounds[j] = Σ_t plan[j][t].
+ *   objective     P1 objective  (1/(N·T)) Σ p_j·L_j − k·max_j makespan_j   shockwave.py:373-379
+ *   utility       the first term alone
+ *   makespan      max_j max(0, R_j − d_j·e_j)                              shockwave.py:260-263, :363
+ *   p2_objective  Σ_{n_j>0} p_j·(Σ_t t·y_jt)/n_j                           shockwave.py:309-322
+ *   bound         an upper bound on the aggregate P1 optimum (fractional-knapsack bound)
+ *   iters         number of level/price evaluations the solver made
+ */
+typedef struct sw_result {
+    uint8_t* plan;
+    int32_t* planned_rounds;
+    double objective;
+    double utility;
+    double makespan;
+    double p2_objective;
+    double bound;
+    int32_t iters;
+    int32_t status;
+} sw_result;
+
+/* Handle creation.  max_* reserve device capacity; 0 picks defaults. */
+typedef struct sw_config {
+    int32_t device;          /* HIP device ordinal                              */
+    int32_t max_instances;   /* instances per batched call                      */
+    int64_t max_total_jobs;  /* Σ num_jobs over a batch                         */
+    int32_t max_jobs_per_instance;
+    void* stream;            /* hipStream_t to launch on; NULL = own stream     */
+} sw_config;
+
+typedef struct sw_handle sw_handle;
+
+int sw_abi_version(void);
+sw_handle* sw_create(const sw_config* cfg);
+void sw_destroy(sw_handle* h);
+const char* sw_last_error(const sw_handle* h);
+/* Message of the last sw_create() failure (no handle exists then). */
+const char* sw_create_error(void);
+
+/*
+ * Single solve, host pointers in and out (synchronous).  Replaces the two
+ * problem.solve() calls of shockwave.py:381 and :323 plus the read-back at
+ * :390-398.
+ */
+int sw_plan_solve(sw_handle* h, const sw_problem* prob, sw_result* res);
+
+/*
+ * Batched solve of `count` independent problems (seed × cluster-size sweeps).
+ * Host pointers; synchronous.  results[i] must point to caller buffers sized
+ * for problems[i].
+ */
+int sw_plan_solve_batch(sw_handle* h, int32_t count, const sw_problem* problems,
+                        sw_result* results);
+
+/*
+ * Device-resident batch (inputs already in HBM, for benchmarking and for
+ * callers that keep the SoA on the GPU):
+ *   sw_batch_upload   copies `count` problems into the handle's device SoA;
+ *   sw_batch_run      enqueues the solve kernels on the handle's stream
+ *                     (asynchronous, no host sync, graph-capturable);
+ *   sw_batch_download synchronises and copies plans/results back.
+ */
+int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* problems);
+int sw_batch_run(sw_handle* h);
+int sw_batch_download(sw_handle* h, sw_result* results);
+
+/* The HIP stream the handle launches on (hipStream_t as void*). */
+void* sw_stream(sw_handle* h);
+
+/*
+ * Per-kernel timing with HIP events recorded on the handle's stream around
+ * each launch of sw_batch_run.  enable=1 turns it on (adds two event records
+ * per kernel).  sw_kernel_times() synchronises and returns accumulated ms for
+ * [0] the row-build kernel and [1] the plan kernel, plus the number of runs.
+ */
+int sw_set_timing(sw_handle* h, int32_t enable);
+int sw_kernel_times(sw_handle* h, double* ms_rows, double* ms_plan, int32_t* runs);
+
+/*
+ * Sharded single instance (jobs split across ranks, one process per GPU).
+ * The aggregate weight/count reductions of every price/level step are summed
+ * across ranks with ncclAllReduce over xGMI.  unique_id points to
+ * SW_NCCL_UNIQUE_ID_BYTES bytes produced by sw_dist_unique_id() on rank 0 and
+ * broadcast by the caller.  prob describes this rank's slice of jobs
+ * (num_jobs = local count); job_offset/total_jobs place the slice globally.
+ * res->plan / planned_rounds receive this rank's rows; scalar results are
+ * global and identical on every rank.
+ */
+#define SW_NCCL_UNIQUE_ID_BYTES 128
+int sw_dist_unique_id(void* out_bytes);
+int sw_dist_init(sw_handle* h, const void* unique_id, int32_t rank, int32_t world);
+int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset,
+                       int64_t total_jobs, sw_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SHOCKWAVE_AMD_H */

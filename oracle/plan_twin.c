@@ -1,0 +1,497 @@
+/*
+ * oracle/plan_twin.c — TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+ *
+ * Sequential CPU restatement of the deterministic plan algorithm that the HIP
+ * kernel in shockwave-replication_amd/csrc/sw_kernels.hip implements
+ * (DESIGN.md §3).  Its job is to be the bit-exact checker the north star asks
+ * for ("the rounding of the relaxed plan into a per-round job→worker
+ * schedule, deterministic and bit-exact vs a CPU reimplementation").  It is
+ * NOT the restatement of the reference solver — that is oracle/milp_ref.py
+ * (HiGHS MILP of shockwave.py:330-388 / :281-328) — and it is never linked
+ * into, loaded by, or used as a fallback for the product path.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Reference semantics it follows (through the per-job reduction in
+ * sw_arith.h): P1 = shockwave.py:330-388, P2 = shockwave.py:281-328,
+ * schedule read-back = shockwave.py:390-398.
+ *
+ * Bit-exactness contract with the GPU:
+ *   - per-job arithmetic is the shared sw_arith.h, -ffp-contract=off on both;
+ *   - every float sum over jobs is sw_detsum (1024 contiguous chunks summed
+ *     left to right, then a halving tree) — the GPU plan kernel runs exactly
+ *     1024 threads per instance and reduces in the same order;
+ *   - integer sums, maxima and lexicographic arg-max are order independent.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/shockwave_amd.h"
+#include "../shockwave-replication_amd/csrc/sw_arith.h"
+#include "../shockwave-replication_amd/csrc/sw_validate.h"
+
+typedef struct {
+    int32_t N, T, G, nb;
+    int64_t C;
+    double k, A;
+    const double* beta;
+    const double* ell;
+    sw_jobc* jc;
+    int32_t* Tj; /* rounds job j may use: T, or 0 if w_j > G (shockwave.py:64-75) */
+    float* key;  /* [N][T] */
+    int64_t passes;
+} twin_t;
+
+#define K_(P, j, n) ((P)->key[(size_t)(j) * (P)->T + (n)])
+
+/* Deterministic sum: SW_DET_LANES contiguous chunks, then a halving tree. */
+static double sw_detsum(const double* v, int32_t N) {
+    double part[SW_DET_LANES];
+    int32_t q = (N + SW_DET_LANES - 1) / SW_DET_LANES;
+    for (int32_t lane = 0; lane < SW_DET_LANES; ++lane) {
+        double s = 0.0;
+        int32_t lo = lane * q, hi = lo + q < N ? lo + q : N;
+        for (int32_t j = lo; j < hi; ++j) s = s + v[j];
+        part[lane] = s;
+    }
+    for (int32_t h = SW_DET_LANES / 2; h >= 1; h >>= 1)
+        for (int32_t i = 0; i < h; ++i) part[i] = part[i] + part[i + h];
+    return part[0];
+}
+
+static double fval(const twin_t* P, int32_t j, int32_t n) {
+    return sw_f(&P->jc[j], n, P->nb, P->beta, P->ell);
+}
+
+static int32_t lforce(const twin_t* P, int32_t j, double M) {
+    int32_t c = 0;
+    for (int32_t n = 0; n < P->Tj[j]; ++n) c += (sw_g(&P->jc[j], n) > M);
+    return c;
+}
+
+static int32_t cnt_gt(const twin_t* P, int32_t j, uint32_t rho, int32_t l) {
+    int32_t c = 0;
+    for (int32_t n = l; n < P->Tj[j]; ++n) c += (sw_fbits_of(K_(P, j, n)) > rho);
+    return c;
+}
+
+static int32_t cnt_ge(const twin_t* P, int32_t j, uint32_t rho, int32_t l) {
+    int32_t c = 0;
+    for (int32_t n = l; n < P->Tj[j]; ++n) c += (sw_fbits_of(K_(P, j, n)) >= rho);
+    return c;
+}
+
+typedef struct {
+    double U, Mact, J, ubound;
+} sel_eval_t;
+
+/*
+ * SELECT(M): forced prefix l_j = #{n<T : g_j(n) > M}, then the greedy over
+ * the remaining increments in key order (key desc, j asc, n asc) with budget
+ * C − Σ w l, computed as a price threshold ρ* (bisection over fp32 key bits),
+ * the job-ordered tie group at ρ*, and a ≤7-unit width tail.  is_inf: M = +∞.
+ */
+static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
+                        int32_t* taken, double* tmp, sel_eval_t* ev) {
+    const int32_t N = P->N, T = P->T;
+    int64_t Wf = 0, Wall = 0;
+    for (int32_t j = 0; j < N; ++j) {
+        l[j] = is_inf ? 0 : lforce(P, j, M);
+        Wf += (int64_t)P->jc[j].w * l[j];
+        Wall += (int64_t)P->jc[j].w * (P->Tj[j] - l[j]);
+    }
+    P->passes++;
+    if (Wf > P->C) return -1;
+    int64_t bud = P->C - Wf;
+    double rho_d = 0.0;
+    int64_t wgt_star = 0;
+    if (Wall <= bud) {
+        for (int32_t j = 0; j < N; ++j) { n[j] = P->Tj[j]; taken[j] = P->Tj[j] - l[j]; }
+        wgt_star = Wall;
+    } else {
+        uint32_t lo = 0, hi = SW_KEY_INF_BITS;
+        while (lo < hi) {
+            uint32_t mid = lo + ((hi - lo) >> 1);
+            int64_t wg = 0;
+            for (int32_t j = 0; j < N; ++j) wg += (int64_t)P->jc[j].w * cnt_gt(P, j, mid, l[j]);
+            P->passes++;
+            if (wg <= bud) hi = mid; else lo = mid + 1;
+        }
+        uint32_t rho = lo;
+        rho_d = (double)sw_float_of(rho);
+        int64_t wt = 0;
+        for (int32_t j = 0; j < N; ++j) {
+            taken[j] = cnt_gt(P, j, rho, l[j]);
+            wt += (int64_t)P->jc[j].w * taken[j];
+        }
+        wgt_star = wt;
+        int64_t rem = bud - wt;
+        /* tie group (key == ρ*) taken in job order */
+        int64_t excl = 0, used = 0;
+        for (int32_t j = 0; j < N; ++j) {
+            int32_t tie = cnt_ge(P, j, rho, l[j]) - taken[j];
+            int64_t wj = P->jc[j].w;
+            int32_t tt;
+            if (excl + wj * tie <= rem) tt = tie;
+            else if (excl <= rem) tt = (int32_t)((rem - excl) / wj);
+            else tt = 0;
+            n[j] = l[j] + taken[j] + tt;
+            used += wj * tt;
+            excl += wj * tie;
+        }
+        P->passes++;
+        int64_t rem2 = rem - used;
+        /* width tail: next item in key order among jobs that still fit */
+        while (rem2 > 0) {
+            int32_t best = -1;
+            uint32_t bk = 0;
+            for (int32_t j = 0; j < N; ++j) {
+                if (n[j] < P->Tj[j] && (int64_t)P->jc[j].w <= rem2) {
+                    uint32_t kb = sw_fbits_of(K_(P, j, n[j]));
+                    if (best < 0 || kb > bk) { best = j; bk = kb; }
+                }
+            }
+            P->passes++;
+            if (best < 0) break;
+            n[best] += 1;
+            rem2 -= P->jc[best].w;
+        }
+    }
+    double Mact = 0.0;
+    for (int32_t j = 0; j < N; ++j) {
+        tmp[j] = fval(P, j, n[j]);
+        double gj = sw_g(&P->jc[j], n[j]);
+        Mact = gj > Mact ? gj : Mact;
+    }
+    ev->U = sw_detsum(tmp, N);
+    ev->Mact = Mact;
+    ev->J = ev->U - P->k * Mact;
+    /* Lagrangian bound of the concave relaxation at price ρ*·A */
+    for (int32_t j = 0; j < N; ++j) tmp[j] = fval(P, j, l[j] + taken[j]);
+    ev->ubound = sw_detsum(tmp, N) + (rho_d * P->A) * (double)(bud - wgt_star);
+    P->passes++;
+    return 0;
+}
+
+static int feasible_level(twin_t* P, double M) {
+    int64_t Wf = 0;
+    for (int32_t j = 0; j < P->N; ++j) Wf += (int64_t)P->jc[j].w * lforce(P, j, M);
+    P->passes++;
+    return Wf <= P->C;
+}
+
+static int64_t levels_between(twin_t* P, double a, double b) {
+    int64_t c = 0;
+    for (int32_t j = 0; j < P->N; ++j)
+        for (int32_t n = 0; n <= P->Tj[j]; ++n) {
+            double v = sw_g(&P->jc[j], n);
+            c += (v > a && v < b);
+        }
+    P->passes++;
+    return c;
+}
+
+/* ---- placement (P1 packing and P2): DESIGN.md §3.3 ----
+ * Jobs are visited in a fixed order: (k1 desc, k2 desc, j asc). */
+typedef struct {
+    uint64_t k1;
+    uint32_t k2;
+    int32_t j;
+} ord_t;
+
+static int ord_cmp(const void* A, const void* B) {
+    const ord_t* a = (const ord_t*)A;
+    const ord_t* b = (const ord_t*)B;
+    if (a->k1 != b->k1) return a->k1 > b->k1 ? -1 : 1;
+    if (a->k2 != b->k2) return a->k2 > b->k2 ? -1 : 1;
+    return (a->j < b->j) ? -1 : (a->j > b->j);
+}
+
+static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const uint32_t* k2,
+                 uint8_t* y, int32_t* placed) {
+    const int32_t N = P->N, T = P->T, G = P->G;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    ord_t* ord = (ord_t*)malloc(sizeof(ord_t) * NN);
+    int32_t* r = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* ww = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint8_t* sel = (uint8_t*)malloc(NN);
+    int32_t A = 0;
+    for (int32_t j = 0; j < N; ++j)
+        if (nin[j] > 0) { ord[A].k1 = k1[j]; ord[A].k2 = k2[j]; ord[A].j = j; ++A; }
+    qsort(ord, (size_t)A, sizeof(ord_t), ord_cmp);
+    for (int32_t i = 0; i < A; ++i) { r[i] = nin[ord[i].j]; ww[i] = P->jc[ord[i].j].w; }
+    memset(y, 0, NN * (size_t)T);
+    int64_t H[SW_TMAX + 1], SH[SW_TMAX + 1], need[SW_TMAX];
+    for (int32_t t = 0; t < T; ++t) {
+        int32_t R = T - t;
+        int64_t cap = G;
+        for (int32_t v = 0; v <= R; ++v) { H[v] = 0; SH[v] = 0; }
+        for (int32_t i = 0; i < A; ++i) H[r[i] < R ? r[i] : R] += ww[i];
+        for (int32_t m = 0; m < R; ++m) {
+            int64_t D = 0;
+            for (int32_t v = m + 1; v <= R; ++v) D += H[v] * (int64_t)(v - m);
+            need[m] = D - (int64_t)G * (R - 1 - m);
+        }
+        memset(sel, 0, (size_t)(A > 0 ? A : 1));
+        /* tiers: jobs with more than m rounds left must shed enough now */
+        for (int32_t m = R - 1; m >= 0; --m) {
+            int64_t red = 0;
+            for (int32_t v = m + 1; v <= R; ++v) red += SH[v];
+            int64_t q = need[m] - red;
+            if (q <= 0) continue;
+            int64_t excl = 0, took = 0;
+            for (int32_t i = 0; i < A; ++i) {
+                int32_t rr = r[i] < R ? r[i] : R;
+                if (sel[i] || rr <= m) continue;
+                if (excl < q && excl + ww[i] <= cap) {
+                    sel[i] = 1; SH[rr] += ww[i]; took += ww[i];
+                }
+                excl += ww[i];
+            }
+            cap -= took;
+        }
+        /* fill the rest of the round in order */
+        {
+            int64_t excl = 0, took = 0;
+            for (int32_t i = 0; i < A; ++i) {
+                if (sel[i] || r[i] <= 0) continue;
+                if (excl + ww[i] <= cap) { sel[i] = 1; took += ww[i]; }
+                excl += ww[i];
+            }
+            cap -= took;
+        }
+        /* width tail */
+        while (cap > 0) {
+            int32_t pick = -1;
+            for (int32_t i = 0; i < A; ++i)
+                if (!sel[i] && r[i] > 0 && ww[i] <= cap) { pick = i; break; }
+            if (pick < 0) break;
+            sel[pick] = 1; cap -= ww[pick];
+        }
+        for (int32_t i = 0; i < A; ++i)
+            if (sel[i]) { y[(size_t)ord[i].j * T + t] = 1; r[i] -= 1; }
+    }
+    for (int32_t j = 0; j < N; ++j) placed[j] = 0;
+    for (int32_t i = 0; i < A; ++i) placed[ord[i].j] = nin[ord[i].j] - r[i];
+    free(ord); free(r); free(ww); free(sel);
+}
+
+static void build(twin_t* P, const sw_problem* pr) {
+    const int32_t N = pr->num_jobs, T = pr->future_rounds;
+    P->N = N; P->T = T; P->G = pr->num_gpus; P->nb = pr->num_bases;
+    P->C = (int64_t)pr->num_gpus * T;
+    P->k = pr->regularizer;
+    P->beta = pr->bases; P->ell = pr->log_bases;
+    P->passes = 0;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    P->jc = (sw_jobc*)malloc(sizeof(sw_jobc) * NN);
+    P->key = (float*)malloc(sizeof(float) * NN * T);
+    P->Tj = (int32_t*)malloc(sizeof(int32_t) * NN);
+    double A = 0.0;
+    for (int32_t j = 0; j < N; ++j) {
+        P->jc[j] = sw_make_jobc(N, T, pr->round_duration, pr->nworkers[j], pr->epoch_duration[j],
+                                pr->completed_epochs[j], pr->total_epochs[j],
+                                pr->remaining_runtime[j], pr->priority[j]);
+        A = P->jc[j].a > A ? P->jc[j].a : A;
+        P->Tj[j] = pr->nworkers[j] <= pr->num_gpus ? T : 0;
+    }
+    P->A = A;
+    for (int32_t j = 0; j < N; ++j) {
+        double prev = fval(P, j, 0), vm = 0.0;
+        for (int32_t n = 0; n < T; ++n) {
+            double cur = fval(P, j, n + 1);
+            double v = sw_pos(cur - prev);
+            vm = (n == 0) ? v : sw_min(vm, v);
+            K_(P, j, n) = sw_key(vm, P->jc[j].w, A);
+            prev = cur;
+        }
+    }
+}
+
+/* Level search over the makespan M.  Writes the best
+ * counts to nb, returns the upper bound U∞bound − k·M_lo. */
+static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32_t* tk,
+                           double* tmp) {
+    const int32_t N = P->N;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    sel_eval_t ev, best;
+    select_level(P, 0.0, 1, n, l, tk, tmp, &ev);
+    best = ev;
+    double U_inf = ev.U, M_free = ev.Mact, ubound_inf = ev.ubound;
+    memcpy(nb, n, sizeof(int32_t) * NN);
+    double M_lo = M_free;
+    if (N > 0 && P->k > 0.0) {
+        double lb = 0.0;
+        for (int32_t j = 0; j < N; ++j) lb = sw_max(lb, sw_g(&P->jc[j], P->Tj[j]));
+        uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
+        while (lo < hi) {
+            uint64_t mid = lo + ((hi - lo) >> 1);
+            if (feasible_level(P, sw_from_bits(mid))) hi = mid; else lo = mid + 1;
+        }
+        M_lo = sw_from_bits(lo);
+        select_level(P, M_lo, 0, n, l, tk, tmp, &ev);
+        if (ev.J > best.J || (ev.J == best.J && ev.Mact < best.Mact)) {
+            best = ev; memcpy(nb, n, sizeof(int32_t) * NN);
+        }
+        double width = (U_inf - ev.U) / P->k;
+        double a = M_lo, b = sw_min(M_free, M_lo + width);
+        for (int it = 0; it < SW_GS_ITERS; ++it) {
+            if (!(a < b)) break;
+            if (levels_between(P, a, b) == 0) break;
+            double m1 = a + (b - a) * SW_GS_A;
+            double m2 = a + (b - a) * SW_GS_B;
+            sel_eval_t e1, e2;
+            select_level(P, m1, 0, n, l, tk, tmp, &e1);
+            if (e1.J > best.J || (e1.J == best.J && e1.Mact < best.Mact)) {
+                best = e1; memcpy(nb, n, sizeof(int32_t) * NN);
+            }
+            select_level(P, m2, 0, n, l, tk, tmp, &e2);
+            if (e2.J > best.J || (e2.J == best.J && e2.Mact < best.Mact)) {
+                best = e2; memcpy(nb, n, sizeof(int32_t) * NN);
+            }
+            if (e1.J >= e2.J) b = m2; else a = m1;
+        }
+    }
+    return ubound_inf - P->k * M_lo;
+}
+
+/* Full plan solve; same contract as sw_plan_solve in include/shockwave_amd.h. */
+int twin_plan_solve(const sw_problem* pr, sw_result* res) {
+    if (sw_validate_problem(pr) != 0) return SW_ERR_INVALID;
+    const int32_t N = pr->num_jobs, T = pr->future_rounds;
+    twin_t P;
+    build(&P, pr);
+    size_t NN = N > 0 ? (size_t)N : 1;
+    int32_t* n = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* nb = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* l = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* tk = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* placed = (int32_t*)malloc(sizeof(int32_t) * NN);
+    double* tmp = (double*)malloc(sizeof(double) * NN);
+    uint8_t* y1 = (uint8_t*)malloc(NN * T);
+    uint8_t* y2 = (uint8_t*)malloc(NN * T);
+
+    /* ---- P1: level search + packing, re-solved on a smaller budget when
+     *      widths fragment the rounds ---- */
+    int32_t status = 0;
+    uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
+    uint32_t* k2 = (uint32_t*)malloc(sizeof(uint32_t) * NN);
+    int32_t* nbest = (int32_t*)malloc(sizeof(int32_t) * NN);
+    double bound = 0.0, Jbest = 0.0;
+    for (int it = 0; it < SW_REPACK_ITERS; ++it) {
+        double b0 = level_search(&P, n, nb, l, tk, tmp);
+        if (it == 0) bound = b0;
+        double Mb = 0.0;
+        for (int32_t j = 0; j < N; ++j) Mb = sw_max(Mb, sw_g(&P.jc[j], nb[j]));
+        for (int32_t j = 0; j < N; ++j) {
+            if (nb[j] > 0) {
+                double lvl = sw_g(&P.jc[j], nb[j] - 1);
+                k1[j] = lvl > Mb ? sw_bits(lvl) : 0;
+                k2[j] = sw_fbits_of(K_(&P, j, nb[j] - 1));
+            } else {
+                k1[j] = 0; k2[j] = 0;
+            }
+        }
+        pack(&P, nb, k1, k2, y1, placed);
+        int64_t deficit = 0;
+        for (int32_t j = 0; j < N; ++j) deficit += (int64_t)P.jc[j].w * (nb[j] - placed[j]);
+        double Mp = 0.0;
+        for (int32_t j = 0; j < N; ++j) {
+            tmp[j] = fval(&P, j, placed[j]);
+            Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
+        }
+        double Jp = sw_detsum(tmp, N) - P.k * Mp;
+        P.passes++;
+        if (it == 0 || Jp > Jbest) {
+            Jbest = Jp;
+            memcpy(nbest, placed, sizeof(int32_t) * NN);
+            memcpy(y2, y1, NN * (size_t)T);
+        }
+        if (deficit == 0) break;
+        status |= SW_STATUS_P1_REPACKED;
+        P.C -= deficit;
+    }
+    memcpy(nb, nbest, sizeof(int32_t) * NN);
+    memcpy(y1, y2, NN * (size_t)T); /* y1 = best P1 plan */
+    /* ---- P2: priority placement of the same counts (shockwave.py:281-328) ---- */
+    for (int32_t j = 0; j < N; ++j) {
+        k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] / (double)nb[j]) : 0;
+        k2[j] = 0;
+    }
+    pack(&P, nb, k1, k2, y2, placed);
+    int ok2 = 1;
+    for (int32_t j = 0; j < N; ++j) ok2 &= (placed[j] == nb[j]);
+    uint8_t* yf = y2;
+    if (!ok2) { yf = y1; status |= SW_STATUS_P2_FALLBACK; }
+    free(k1); free(k2); free(nbest);
+    int any = 0;
+    for (int32_t j = 0; j < N; ++j) {
+        int32_t c = 0;
+        for (int32_t t = 0; t < T; ++t) c += yf[(size_t)j * T + t];
+        nb[j] = c;
+        any |= (c > 0);
+    }
+    if (!any) status |= SW_STATUS_NO_PLANNED;
+    double Mact = 0.0;
+    for (int32_t j = 0; j < N; ++j) {
+        tmp[j] = fval(&P, j, nb[j]);
+        Mact = sw_max(Mact, sw_g(&P.jc[j], nb[j]));
+    }
+    double U = sw_detsum(tmp, N);
+    for (int32_t j = 0; j < N; ++j) {
+        if (nb[j] > 0) {
+            int64_t S = 0;
+            for (int32_t t = 0; t < T; ++t) S += (int64_t)t * yf[(size_t)j * T + t];
+            tmp[j] = ((double)S / (double)nb[j]) * pr->priority[j];
+        } else {
+            tmp[j] = 0.0;
+        }
+    }
+    res->p2_objective = sw_detsum(tmp, N);
+    res->utility = U;
+    res->makespan = Mact;
+    res->objective = U - P.k * Mact;
+    res->bound = bound;
+    res->iters = (int32_t)P.passes;
+    res->status = status;
+    if (res->plan && N > 0) memcpy(res->plan, yf, (size_t)N * T);
+    if (res->planned_rounds && N > 0) memcpy(res->planned_rounds, nb, sizeof(int32_t) * (size_t)N);
+    free(P.jc); free(P.key); free(P.Tj); free(n); free(nb); free(l); free(tk);
+    free(placed); free(tmp); free(y1); free(y2);
+    return (status & SW_STATUS_P2_FALLBACK) ? SW_FALLBACK : SW_OK;
+}
+
+/* Exposed for tests: the per-job f, g rows (n = 0..T) and fp32 keys (n < T). */
+int twin_job_rows(const sw_problem* pr, double* f, double* g, float* key) {
+    if (sw_validate_problem(pr) != 0) return SW_ERR_INVALID;
+    twin_t P;
+    build(&P, pr);
+    const int32_t N = pr->num_jobs, T = pr->future_rounds;
+    for (int32_t j = 0; j < N; ++j) {
+        for (int32_t n = 0; n <= T; ++n) {
+            f[(size_t)j * (T + 1) + n] = fval(&P, j, n);
+            g[(size_t)j * (T + 1) + n] = sw_g(&P.jc[j], n);
+        }
+        for (int32_t n = 0; n < T; ++n) key[(size_t)j * T + n] = K_(&P, j, n);
+    }
+    free(P.jc); free(P.key); free(P.Tj);
+    return 0;
+}
+
+/* Exposed for tests: objective of given planned-round counts (no packing). */
+double twin_eval_counts(const sw_problem* pr, const int32_t* ncount, double* makespan) {
+    twin_t P;
+    build(&P, pr);
+    const int32_t N = pr->num_jobs;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    double* tmp = (double*)malloc(sizeof(double) * NN);
+    double M = 0.0;
+    for (int32_t j = 0; j < N; ++j) {
+        tmp[j] = fval(&P, j, ncount[j]);
+        M = sw_max(M, sw_g(&P.jc[j], ncount[j]));
+    }
+    double U = sw_detsum(tmp, N);
+    if (makespan) *makespan = M;
+    free(P.jc); free(P.key); free(P.Tj); free(tmp);
+    return U - pr->regularizer * M;
+}

@@ -1,0 +1,60 @@
+/*
+ * sw_device.h — device-side batch layout shared by sw_kernels.hip and the
+ * host API (sw_api.hip).
+ *
+ * HBM layout (structure of arrays, one batch of independent instances):
+ *   per-job inputs      w[int32] d[f64] F[int32] E[int32] R[f64] p[f64]
+ *                       concatenated over instances (instance i starts at
+ *                       inst[i].job_off)
+ *   plan bytes          [Σ_i N_i·T_i] row-major per instance ([N_i][T_i])
+ *   planned rounds      [Σ_i N_i] int32
+ *   per-instance out    sw_out_dev
+ *   workspace (only for instances with N > SW_LDS_JOBS): per-job state,
+ *                       fp32 key rows [job][KT], masks, sort keys.
+ */
+#pragma once
+#include <stdint.h>
+
+#include "sw_arith.h"
+
+#define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip */
+
+struct sw_inst_dev {
+    int32_t N, T, G, nb;
+    int64_t job_off;
+    int64_t plan_off;
+    double delta, k;
+    double beta[SW_BMAX];
+    double ell[SW_BMAX];
+};
+
+struct sw_out_dev {
+    double objective, utility, makespan, p2_objective, bound;
+    int32_t iters, status;
+};
+
+/* Global workspace, per job (used only when N > SW_LDS_JOBS). */
+struct sw_ws_dev {
+    uint8_t* u8;    /* [total_jobs][SW_WS_U8]      */
+    uint64_t* u64;  /* [total_jobs][3] masks        */
+    uint64_t* sort; /* [2·total_jobs][2] sort keys  */
+    float* keys;    /* [total_jobs][KT]             */
+    sw_jobc* jc;    /* [total_jobs]                 */
+};
+#define SW_WS_U8 12
+
+struct sw_batch_dev {
+    const sw_inst_dev* inst;
+    int32_t count;
+    int32_t KT;
+    const int32_t* w;
+    const double* d;
+    const int32_t* F;
+    const int32_t* E;
+    const double* R;
+    const double* p;
+    uint8_t* plan;
+    int32_t* planned;
+    sw_out_dev* out;
+    sw_ws_dev ws;
+};

@@ -1,0 +1,306 @@
+"""ctypes binding of the C-ABI in include/shockwave_amd.h.
+
+This is the only way the host mirror reaches the solver: there is no Python
+or CPU fallback.  If ``libshockwave_amd.so`` is missing or was built without
+HIP the loader raises, so a product call can never silently run elsewhere.
+
+The structs mirror include/shockwave_amd.h field for field.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libshockwave_amd.so"
+LIB_PATH = os.path.join(_HERE, "lib", LIB_NAME)
+
+SW_OK = 0
+SW_FALLBACK = 1
+SW_ERR_INVALID = -1
+SW_ERR_HIP = -2
+SW_ERR_CAPACITY = -3
+SW_ERR_RCCL = -4
+SW_ERR_NOT_BUILT = -5
+
+SW_STATUS_P1_REPACKED = 0x1
+SW_STATUS_P2_FALLBACK = 0x2
+SW_STATUS_NO_PLANNED = 0x4
+
+SW_MAX_ROUNDS = 64
+SW_MAX_BASES = 8
+SW_NCCL_UNIQUE_ID_BYTES = 128
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+_up = C.POINTER(C.c_uint8)
+
+
+class SwProblem(C.Structure):
+    _fields_ = [
+        ("num_jobs", C.c_int32),
+        ("future_rounds", C.c_int32),
+        ("num_gpus", C.c_int32),
+        ("num_bases", C.c_int32),
+        ("round_duration", C.c_double),
+        ("regularizer", C.c_double),
+        ("bases", _dp),
+        ("log_bases", _dp),
+        ("nworkers", _ip),
+        ("epoch_duration", _dp),
+        ("completed_epochs", _ip),
+        ("total_epochs", _ip),
+        ("remaining_runtime", _dp),
+        ("priority", _dp),
+    ]
+
+
+class SwResult(C.Structure):
+    _fields_ = [
+        ("plan", _up),
+        ("planned_rounds", _ip),
+        ("objective", C.c_double),
+        ("utility", C.c_double),
+        ("makespan", C.c_double),
+        ("p2_objective", C.c_double),
+        ("bound", C.c_double),
+        ("iters", C.c_int32),
+        ("status", C.c_int32),
+    ]
+
+
+class SwConfig(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("max_instances", C.c_int32),
+        ("max_total_jobs", C.c_int64),
+        ("max_jobs_per_instance", C.c_int32),
+        ("stream", C.c_void_p),
+    ]
+
+
+def log_bases(bases):
+    """shockwave.py:99-105 — log(β_b), with log(0) replaced by log(1e-6)."""
+    return [math.log(1e-6) if b == 0.0 else math.log(b) for b in bases]
+
+
+class ProblemArrays:
+    """Owns the contiguous numpy arrays behind one SwProblem (and its result).
+
+    Fields follow include/shockwave_amd.h; see there for the reference line of
+    each one.
+    """
+
+    def __init__(self, nworkers, epoch_duration, completed_epochs, total_epochs,
+                 remaining_runtime, priority, future_rounds, num_gpus, round_duration,
+                 regularizer, bases=(0.0, 0.2, 0.4, 0.6, 0.8, 1.0)):
+        self.w = np.ascontiguousarray(nworkers, dtype=np.int32)
+        self.d = np.ascontiguousarray(epoch_duration, dtype=np.float64)
+        self.F = np.ascontiguousarray(completed_epochs, dtype=np.int32)
+        self.E = np.ascontiguousarray(total_epochs, dtype=np.int32)
+        self.R = np.ascontiguousarray(remaining_runtime, dtype=np.float64)
+        self.p = np.ascontiguousarray(priority, dtype=np.float64)
+        self.T = int(future_rounds)
+        self.G = int(num_gpus)
+        self.delta = float(round_duration)
+        self.k = float(regularizer)
+        self.bases = np.ascontiguousarray(bases, dtype=np.float64)
+        self.ell = np.ascontiguousarray(log_bases(list(bases)), dtype=np.float64)
+        n = len(self.w)
+        for a in (self.d, self.F, self.E, self.R, self.p):
+            if len(a) != n:
+                raise ValueError("per-job arrays must have the same length")
+        self.N = n
+        self.plan = np.zeros((n, self.T), dtype=np.uint8)
+        self.planned = np.zeros(n, dtype=np.int32)
+
+    def c_problem(self) -> SwProblem:
+        p = SwProblem()
+        p.num_jobs = self.N
+        p.future_rounds = self.T
+        p.num_gpus = self.G
+        p.num_bases = len(self.bases)
+        p.round_duration = self.delta
+        p.regularizer = self.k
+        p.bases = self.bases.ctypes.data_as(_dp)
+        p.log_bases = self.ell.ctypes.data_as(_dp)
+        p.nworkers = self.w.ctypes.data_as(_ip)
+        p.epoch_duration = self.d.ctypes.data_as(_dp)
+        p.completed_epochs = self.F.ctypes.data_as(_ip)
+        p.total_epochs = self.E.ctypes.data_as(_ip)
+        p.remaining_runtime = self.R.ctypes.data_as(_dp)
+        p.priority = self.p.ctypes.data_as(_dp)
+        return p
+
+    def c_result(self) -> SwResult:
+        r = SwResult()
+        r.plan = self.plan.ctypes.data_as(_up)
+        r.planned_rounds = self.planned.ctypes.data_as(_ip)
+        return r
+
+
+def result_dict(r: SwResult, arrays: ProblemArrays, rc: int) -> dict:
+    return {
+        "rc": rc,
+        "plan": arrays.plan.copy(),
+        "planned_rounds": arrays.planned.copy(),
+        "objective": r.objective,
+        "utility": r.utility,
+        "makespan": r.makespan,
+        "p2_objective": r.p2_objective,
+        "bound": r.bound,
+        "iters": r.iters,
+        "status": r.status,
+    }
+
+
+def declare_solver_api(lib, prefix: str):
+    """Declare argtypes of a library exporting <prefix>plan_solve (product or twin)."""
+    fn = getattr(lib, prefix + "plan_solve")
+    fn.argtypes = [C.POINTER(SwProblem), C.POINTER(SwResult)] if prefix == "twin_" else \
+        [C.c_void_p, C.POINTER(SwProblem), C.POINTER(SwResult)]
+    fn.restype = C.c_int
+    return fn
+
+
+# Every symbol include/shockwave_amd.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "sw_abi_version", "sw_create", "sw_destroy", "sw_last_error", "sw_create_error",
+    "sw_plan_solve", "sw_plan_solve_batch", "sw_batch_upload", "sw_batch_run",
+    "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
+    "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve",
+)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def load(path: str | None = None):
+    """Load libshockwave_amd.so (raises NativeError if it is absent)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NativeError(
+            f"{p} not found: build it with `python __graft_entry__.py build` "
+            "(there is no CPU fallback for the plan solver)")
+    lib = C.CDLL(p)
+    lib.sw_abi_version.restype = C.c_int
+    lib.sw_create.argtypes = [C.POINTER(SwConfig)]
+    lib.sw_create.restype = C.c_void_p
+    lib.sw_destroy.argtypes = [C.c_void_p]
+    lib.sw_destroy.restype = None
+    lib.sw_last_error.argtypes = [C.c_void_p]
+    lib.sw_last_error.restype = C.c_char_p
+    lib.sw_create_error.argtypes = []
+    lib.sw_create_error.restype = C.c_char_p
+    lib.sw_plan_solve.argtypes = [C.c_void_p, C.POINTER(SwProblem), C.POINTER(SwResult)]
+    lib.sw_plan_solve.restype = C.c_int
+    lib.sw_plan_solve_batch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(SwProblem),
+                                        C.POINTER(SwResult)]
+    lib.sw_plan_solve_batch.restype = C.c_int
+    lib.sw_batch_upload.argtypes = [C.c_void_p, C.c_int32, C.POINTER(SwProblem)]
+    lib.sw_batch_upload.restype = C.c_int
+    lib.sw_batch_run.argtypes = [C.c_void_p]
+    lib.sw_batch_run.restype = C.c_int
+    lib.sw_batch_download.argtypes = [C.c_void_p, C.POINTER(SwResult)]
+    lib.sw_batch_download.restype = C.c_int
+    lib.sw_stream.argtypes = [C.c_void_p]
+    lib.sw_stream.restype = C.c_void_p
+    lib.sw_set_timing.argtypes = [C.c_void_p, C.c_int32]
+    lib.sw_set_timing.restype = C.c_int
+    lib.sw_kernel_times.argtypes = [C.c_void_p, _dp, _dp, _ip]
+    lib.sw_kernel_times.restype = C.c_int
+    lib.sw_dist_unique_id.argtypes = [C.c_void_p]
+    lib.sw_dist_unique_id.restype = C.c_int
+    lib.sw_dist_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+    lib.sw_dist_init.restype = C.c_int
+    lib.sw_dist_plan_solve.argtypes = [C.c_void_p, C.POINTER(SwProblem), C.c_int64, C.c_int64,
+                                       C.POINTER(SwResult)]
+    lib.sw_dist_plan_solve.restype = C.c_int
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+class Solver:
+    """One device handle (sw_create / sw_destroy)."""
+
+    def __init__(self, device=0, max_instances=1, max_total_jobs=0, max_jobs_per_instance=0,
+                 stream=None, lib=None):
+        self.lib = lib or load()
+        cfg = SwConfig(int(device), int(max_instances), int(max_total_jobs),
+                       int(max_jobs_per_instance), C.c_void_p(stream) if stream else None)
+        h = self.lib.sw_create(C.byref(cfg))
+        if not h:
+            msg = self.lib.sw_create_error()
+            raise NativeError("sw_create failed: " + (msg.decode() if msg else "?"))
+        self.h = C.c_void_p(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.sw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self) -> str:
+        m = self.lib.sw_last_error(self.h)
+        return m.decode() if m else ""
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise NativeError(f"{what} failed ({rc}): {self.error()}")
+        return rc
+
+    def solve(self, arrays: ProblemArrays) -> dict:
+        prob = arrays.c_problem()
+        res = arrays.c_result()
+        rc = self._check(self.lib.sw_plan_solve(self.h, C.byref(prob), C.byref(res)),
+                         "sw_plan_solve")
+        return result_dict(res, arrays, rc)
+
+    def solve_batch(self, batch: list) -> list:
+        probs = (SwProblem * len(batch))(*[a.c_problem() for a in batch])
+        ress = (SwResult * len(batch))(*[a.c_result() for a in batch])
+        rc = self._check(self.lib.sw_plan_solve_batch(self.h, len(batch), probs, ress),
+                         "sw_plan_solve_batch")
+        return [result_dict(ress[i], a, rc) for i, a in enumerate(batch)]
+
+    # device-resident batch (bench)
+    def upload(self, batch: list):
+        self._probs = (SwProblem * len(batch))(*[a.c_problem() for a in batch])
+        self._batch = batch
+        self._check(self.lib.sw_batch_upload(self.h, len(batch), self._probs), "sw_batch_upload")
+
+    def run(self):
+        self._check(self.lib.sw_batch_run(self.h), "sw_batch_run")
+
+    def download(self) -> list:
+        ress = (SwResult * len(self._batch))(*[a.c_result() for a in self._batch])
+        rc = self._check(self.lib.sw_batch_download(self.h, ress), "sw_batch_download")
+        return [result_dict(ress[i], a, rc) for i, a in enumerate(self._batch)]
+
+    def stream(self) -> int:
+        return self.lib.sw_stream(self.h) or 0
+
+    def set_timing(self, on: bool):
+        self._check(self.lib.sw_set_timing(self.h, 1 if on else 0), "sw_set_timing")
+
+    def kernel_times(self):
+        a, b, n = C.c_double(), C.c_double(), C.c_int32()
+        self._check(self.lib.sw_kernel_times(self.h, C.byref(a), C.byref(b), C.byref(n)),
+                    "sw_kernel_times")
+        return a.value, b.value, n.value
