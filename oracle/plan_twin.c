@@ -370,6 +370,8 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     double* tmp = (double*)malloc(sizeof(double) * NN);
     uint8_t* y1 = (uint8_t*)malloc(NN * T);
     uint8_t* y2 = (uint8_t*)malloc(NN * T);
+    uint8_t* ybest = (uint8_t*)malloc(NN * T);
+    int32_t* placed2 = (int32_t*)malloc(sizeof(int32_t) * NN);
 
     /* ---- P1: level search + packing, re-solved on a smaller budget when
      *      widths fragment the rounds ---- */
@@ -383,36 +385,54 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         if (it == 0) bound = b0;
         double Mb = 0.0;
         for (int32_t j = 0; j < N; ++j) Mb = sw_max(Mb, sw_g(&P.jc[j], nb[j]));
-        for (int32_t j = 0; j < N; ++j) {
-            if (nb[j] > 0) {
-                double lvl = sw_g(&P.jc[j], nb[j] - 1);
-                k1[j] = lvl > Mb ? sw_bits(lvl) : 0;
-                k2[j] = sw_fbits_of(K_(&P, j, nb[j] - 1));
-            } else {
-                k1[j] = 0; k2[j] = 0;
-            }
-        }
-        pack(&P, nb, k1, k2, y1, placed);
+        /* two packing orders: A = (critical level, key), B = (critical level,
+         * width, key); critical = losing the last round raises the makespan
+         * (only meaningful when k > 0).  Keep the better packed plan. */
         int64_t deficit = 0;
-        for (int32_t j = 0; j < N; ++j) deficit += (int64_t)P.jc[j].w * (nb[j] - placed[j]);
-        double Mp = 0.0;
-        for (int32_t j = 0; j < N; ++j) {
-            tmp[j] = fval(&P, j, placed[j]);
-            Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
+        double Jp = 0.0;
+        for (int ord = 0; ord < 2; ++ord) {
+            for (int32_t j = 0; j < N; ++j) {
+                if (nb[j] > 0) {
+                    double lvl = sw_g(&P.jc[j], nb[j] - 1);
+                    int crit = P.k > 0.0 && lvl > Mb;
+                    k1[j] = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (ord ? (uint64_t)P.jc[j].w : 0);
+                    k2[j] = sw_fbits_of(K_(&P, j, nb[j] - 1));
+                } else {
+                    k1[j] = 0; k2[j] = 0;
+                }
+            }
+            pack(&P, nb, k1, k2, ord ? y2 : y1, ord ? placed2 : placed);
+            int64_t dfc = 0;
+            double Mp = 0.0;
+            const int32_t* pl = ord ? placed2 : placed;
+            for (int32_t j = 0; j < N; ++j) {
+                dfc += (int64_t)P.jc[j].w * (nb[j] - pl[j]);
+                tmp[j] = fval(&P, j, pl[j]);
+                Mp = sw_max(Mp, sw_g(&P.jc[j], pl[j]));
+            }
+            double Jo = sw_detsum(tmp, N) - P.k * Mp;
+            P.passes++;
+            if (ord == 0 || Jo > Jp) {
+                Jp = Jo;
+                deficit = dfc;
+                if (ord == 1) {
+                    memcpy(placed, placed2, sizeof(int32_t) * NN);
+                    memcpy(y1, y2, NN * (size_t)T);
+                }
+            }
+            if (ord == 0 && dfc == 0) break; /* order A packed everything */
         }
-        double Jp = sw_detsum(tmp, N) - P.k * Mp;
-        P.passes++;
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             memcpy(nbest, placed, sizeof(int32_t) * NN);
-            memcpy(y2, y1, NN * (size_t)T);
+            memcpy(ybest, y1, NN * (size_t)T);
         }
         if (deficit == 0) break;
         status |= SW_STATUS_P1_REPACKED;
         P.C -= deficit;
     }
     memcpy(nb, nbest, sizeof(int32_t) * NN);
-    memcpy(y1, y2, NN * (size_t)T); /* y1 = best P1 plan */
+    memcpy(y1, ybest, NN * (size_t)T); /* y1 = best P1 plan */
     /* ---- P2: priority placement of the same counts (shockwave.py:281-328) ---- */
     for (int32_t j = 0; j < N; ++j) {
         k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] / (double)nb[j]) : 0;
@@ -457,7 +477,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     if (res->plan && N > 0) memcpy(res->plan, yf, (size_t)N * T);
     if (res->planned_rounds && N > 0) memcpy(res->planned_rounds, nb, sizeof(int32_t) * (size_t)N);
     free(P.jc); free(P.key); free(P.Tj); free(n); free(nb); free(l); free(tk);
-    free(placed); free(tmp); free(y1); free(y2);
+    free(placed); free(placed2); free(tmp); free(y1); free(y2); free(ybest);
     return (status & SW_STATUS_P2_FALLBACK) ? SW_FALLBACK : SW_OK;
 }
 

@@ -130,5 +130,7 @@ SW_HD double sw_pos(double v) { return v > 0.0 ? v : 0.0; }
 #define SW_GS_B 0.6180339887498949
 #define SW_GS_ITERS 32
 #define SW_REPACK_ITERS 3
+/* marks makespan-critical jobs in the P1 packing order key */
+#define SW_CRIT_BIT 0x8000000000000000ULL
 
 #endif /* SW_ARITH_H */

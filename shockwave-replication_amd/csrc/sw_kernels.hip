@@ -55,7 +55,7 @@ struct Ctx {
     const int32_t* w_in;
     const double* p_in;
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
-    uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *nfin;
+    uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
     /* per-position state of the packer */
     uint8_t *rpos, *wpos, *selp;
     int32_t* ordj;
@@ -375,10 +375,10 @@ struct Ctx {
      * MODE 2: P2 order (p_j / n_j desc).  Writes masks y[job], placed[job].
      */
     template <int MODE>
-    __device__ __forceinline__ void pack(const uint8_t* nin, uint64_t* y) {
+    __device__ __forceinline__ void pack(const uint8_t* nin, uint64_t* y, uint8_t* placed_out) {
         __syncthreads();
         double Mb = 0.0;
-        if (MODE == 1) {
+        if (MODE != 2) {
             for (int j = jlo(); j < jhi(); ++j) Mb = sw_max(Mb, gval(j, nin[j]));
             Mb = block_max_d(Mb, S);
         }
@@ -392,9 +392,11 @@ struct Ctx {
             if (nj > 0) {
                 uint64_t k1;
                 uint32_t k2;
-                if (MODE == 1) {
+                if (MODE != 2) {
+                    /* twin: orders A (MODE 1) and B (MODE 3) */
                     double lvl = gval(j, nj - 1);
-                    k1 = lvl > Mb ? sw_bits(lvl) : 0;
+                    bool crit = k > 0.0 && lvl > Mb;
+                    k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (MODE == 3 ? (uint64_t)jc(j).w : 0);
                     k2 = kbits(j, nj - 1);
                 } else {
                     k1 = sw_bits(p_in[j] / (double)nj);
@@ -519,9 +521,9 @@ struct Ctx {
             }
             __syncthreads();
         }
-        for (int j = jlo(); j < jhi(); ++j) placed[j] = 0;
+        for (int j = jlo(); j < jhi(); ++j) placed_out[j] = 0;
         __syncthreads();
-        for (int i = plo; i < phi; ++i) placed[ordj[i]] = (uint8_t)(nin[ordj[i]] - rpos[i]);
+        for (int i = plo; i < phi; ++i) placed_out[ordj[i]] = (uint8_t)(nin[ordj[i]] - rpos[i]);
         __syncthreads();
     }
 };
@@ -570,6 +572,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.tkcur = carve(NJ);
         c.nbest = carve(NJ);
         c.placed = carve(NJ);
+        c.placed2 = carve(NJ);
         c.nfin = carve(NJ);
         c.rpos = carve(NJ);
         c.wpos = carve(NJ);
@@ -600,6 +603,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.rpos = u8 + 6 * (size_t)N;
         c.wpos = u8 + 7 * (size_t)N;
         c.selp = u8 + 8 * (size_t)N;
+        c.placed2 = u8 + 9 * (size_t)N;
         uint64_t* m64 = B.ws.u64 + 4 * jo;
         c.ycur = m64;
         c.ybest = m64 + N;
@@ -623,17 +627,35 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     for (int it = 0; it < SW_REPACK_ITERS; ++it) {
         const double b0 = c.level_search();
         if (it == 0) bound = b0;
-        c.template pack<1>(c.nbest, c.ycur);
-        int64_t def_l = 0;
-        double fs = 0.0, gm = 0.0;
-        for (int j = c.jlo(); j < c.jhi(); ++j) {
-            def_l += (int64_t)c.jc(j).w * (c.nbest[j] - c.placed[j]);
-            fs = fs + c.fval(j, c.placed[j]);
-            gm = sw_max(gm, c.gval(j, c.placed[j]));
+        /* order A; order B only if A left rounds unplaced (twin: ord loop) */
+        int64_t deficit = 0;
+        double Jp = 0.0;
+        for (int ord = 0; ord < 2; ++ord) {
+            uint8_t* pl = ord ? c.placed2 : c.placed;
+            if (ord == 0) c.template pack<1>(c.nbest, c.ycur, pl);
+            else c.template pack<3>(c.nbest, c.y2, pl);
+            int64_t def_l = 0;
+            double fs = 0.0, gm = 0.0;
+            for (int j = c.jlo(); j < c.jhi(); ++j) {
+                def_l += (int64_t)c.jc(j).w * (c.nbest[j] - pl[j]);
+                fs = fs + c.fval(j, pl[j]);
+                gm = sw_max(gm, c.gval(j, pl[j]));
+            }
+            const int64_t dfc = block_sum(def_l, c.S);
+            const double Jo = block_detsum(fs, c.S) - c.k * block_max_d(gm, c.S);
+            c.passes++;
+            if (ord == 0 || Jo > Jp) {
+                Jp = Jo;
+                deficit = dfc;
+                if (ord == 1) {
+                    for (int j = c.jlo(); j < c.jhi(); ++j) {
+                        c.placed[j] = c.placed2[j];
+                        c.ycur[j] = c.y2[j];
+                    }
+                }
+            }
+            if (ord == 0 && dfc == 0) break;
         }
-        const int64_t deficit = block_sum(def_l, c.S);
-        const double Jp = block_detsum(fs, c.S) - c.k * block_max_d(gm, c.S);
-        c.passes++;
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             for (int j = c.jlo(); j < c.jhi(); ++j) {
@@ -646,7 +668,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.C -= deficit;
     }
     /* ---- P2 (twin: priority placement of the same counts) ---- */
-    c.template pack<2>(c.nfin, c.y2);
+    c.template pack<2>(c.nfin, c.y2, c.placed);
     int64_t bad_l = 0;
     for (int j = c.jlo(); j < c.jhi(); ++j) bad_l += (c.placed[j] != c.nfin[j]);
     const bool ok2 = block_sum(bad_l, c.S) == 0;
@@ -707,7 +729,7 @@ extern "C" size_t sw_plan_kernel_lds_bytes(int one) {
                r16(sizeof(int64_t) * 8);
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
-        s += 9 * r16(NJ) + r16(4 * NJ) + 5 * r16(8 * NJ);
+        s += 10 * r16(NJ) + r16(4 * NJ) + 5 * r16(8 * NJ);
     }
     return s;
 }

@@ -60,3 +60,42 @@ def test_gpu_deterministic(gpu_solver):
     r1 = gpu_solver.solve(a)
     r2 = gpu_solver.solve(a)
     assert_same_result(r1, r2, "repeat")
+
+
+EDGE = [
+    dict(),
+    dict(regularizer=0.0),
+    dict(nworkers=[4, 1], num_gpus=2),
+    dict(completed_epochs=[10, 1], priority=[0.0, 2.0], remaining_runtime=[1.0, 150.0]),
+    dict(num_gpus=0),
+    dict(priority=[1e300, 1e-300]),
+]
+
+
+@pytest.mark.parametrize("kw", EDGE, ids=[str(i) for i in range(len(EDGE))])
+def test_gpu_edge_cases_match_twin(kw, gpu_solver, twin):
+    import sw_native as sn
+
+    base = dict(nworkers=[1, 2], epoch_duration=[100.0, 50.0], completed_epochs=[0, 1],
+                total_epochs=[10, 4], remaining_runtime=[1000.0, 150.0], priority=[1.0, 2.0],
+                future_rounds=4, num_gpus=2, round_duration=120.0, regularizer=1.0)
+    base.update(kw)
+    a = sn.ProblemArrays(**base)
+    assert_same_result(gpu_solver.solve(a), twin.solve(a), str(kw))
+
+
+def test_gpu_empty_problem(gpu_solver):
+    import sw_native as sn
+
+    a = sn.ProblemArrays([], [], [], [], [], [], 4, 2, 120.0, 1.0)
+    r = gpu_solver.solve(a)
+    assert r["plan"].shape == (0, 4)
+    assert r["status"] & sn.SW_STATUS_NO_PLANNED
+
+
+def test_gpu_rejects_invalid(gpu_solver):
+    import sw_native as sn
+
+    a = sn.ProblemArrays([0], [1.0], [0], [1], [1.0], [1.0], 4, 2, 120.0, 1.0)
+    with pytest.raises(sn.NativeError):
+        gpu_solver.solve(a)

@@ -1,0 +1,135 @@
+"""Oracle checks (CPU).
+
+1. Pins the HiGHS restatement of the reference MILPs (oracle/milp_ref.py) by
+   exhaustive enumeration of every 0/1 plan on tiny instances — two
+   independent restatements of shockwave.py's P1 must agree.
+2. The plan algorithm (via its CPU twin, bit-identical to the GPU kernel)
+   against the MILP oracle: P1 objective no worse than the reference solve
+   by more than 1e-3 relative (BASELINE.json north star), on the reference's
+   cluster configurations (scale_{64,128,256}gpus.json).
+3. Plans are feasible (per-round capacity, shockwave.py:64-75) and
+   deterministic.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import milp_ref as mr
+import sw_native as sn
+import sw_synth as ss
+from helpers import check_plan_valid, to_oracle
+
+REL_TOL = 1e-3  # north star: NSW objective within 1e-3 relative
+
+
+def tiny_cases():
+    out = []
+    for seed in range(6):
+        N, T, G = (3, 3, 2) if seed % 2 else (4, 3, 3)
+        k = [1e5, 1e-3, 1.0][seed % 3]
+        out.append(ss.synth_problem(seed, N, G, T, 120.0, k, 5.0, width_p=(0.7, 0.3, 0.0, 0.0)))
+    return out
+
+
+@pytest.mark.parametrize("ci", range(6))
+def test_milp_restatement_matches_brute_force(ci):
+    a = tiny_cases()[ci]
+    P = to_oracle(a)
+    best, x = mr.brute_force_p1(P)
+    st, xv, obj, bound, _ = mr.solve_p1(P, rel_gap=1e-9, time_limit=60)
+    assert abs(obj - best) <= 1e-6 * max(1.0, abs(best)), (obj, best)
+    n = (xv > 0.5).sum(axis=1)
+    assert abs(mr.evaluate_counts(P, n)[0] - best) <= 1e-6 * max(1.0, abs(best))
+
+
+@pytest.mark.parametrize("ci", range(6))
+def test_twin_matches_brute_force_tiny(ci, twin):
+    a = tiny_cases()[ci]
+    P = to_oracle(a)
+    best, _ = mr.brute_force_p1(P)
+    r = twin.solve(a)
+    check_plan_valid(a, r)
+    got = mr.evaluate_counts(P, r["planned_rounds"])[0]
+    assert got >= best - REL_TOL * abs(best), (got, best)
+
+
+REALISTIC = [(s, N, G) for s in range(3) for N in (50, 120) for G in (32, 64, 128, 256)]
+
+
+@pytest.mark.parametrize("case", REALISTIC, ids=[f"s{s}_N{N}_G{G}" for s, N, G in REALISTIC])
+def test_twin_objective_parity_vs_reference_milp(case, twin):
+    seed, N, G = case
+    cfg = ss.CLUSTER_CONFIG[G]
+    a = ss.synth_problem(seed, N, G, cfg["T"], 120.0, cfg["k"], cfg["lam"])
+    P = to_oracle(a)
+    sol = mr.plan_solve(P, rel_gap=1e-4, time_limit=60)
+    ref = mr.evaluate_counts(P, sol.n)[0]
+    r = twin.solve(a)
+    check_plan_valid(a, r)
+    got, util, mk = mr.evaluate_counts(P, r["planned_rounds"])
+    assert got >= ref - REL_TOL * abs(ref), (got, ref)
+    # the library's own objective equals the independent evaluation
+    assert math.isclose(r["objective"], got, rel_tol=1e-9, abs_tol=1e-9)
+    assert math.isclose(r["makespan"], mk, rel_tol=1e-12, abs_tol=1e-9)
+
+
+def test_twin_deterministic(twin):
+    a = ss.c3_problem(1)
+    r1, r2 = twin.solve(a), twin.solve(a)
+    assert np.array_equal(r1["plan"], r2["plan"]) and r1["objective"] == r2["objective"]
+
+
+def test_c3_plan_valid_and_bounded(twin):
+    a = ss.c3_problem(0)
+    r = twin.solve(a)
+    check_plan_valid(a, r)
+    assert r["objective"] <= r["bound"] + 1e-9 * abs(r["bound"])
+
+
+# --- edge cases the reference model admits ---------------------------------
+def _arr(**kw):
+    base = dict(nworkers=[1, 2], epoch_duration=[100.0, 50.0], completed_epochs=[0, 1],
+                total_epochs=[10, 4], remaining_runtime=[1000.0, 150.0], priority=[1.0, 2.0],
+                future_rounds=4, num_gpus=2, round_duration=120.0, regularizer=1.0)
+    base.update(kw)
+    return sn.ProblemArrays(**base)
+
+
+def test_empty_problem(twin):
+    a = _arr(nworkers=[], epoch_duration=[], completed_epochs=[], total_epochs=[],
+             remaining_runtime=[], priority=[])
+    r = twin.solve(a)
+    assert r["plan"].shape == (0, 4) and r["status"] & sn.SW_STATUS_NO_PLANNED
+
+
+def test_job_wider_than_cluster_never_scheduled(twin):
+    a = _arr(nworkers=[4, 1], num_gpus=2)
+    r = twin.solve(a)
+    assert r["planned_rounds"][0] == 0
+    check_plan_valid(a, r)
+
+
+def test_zero_regularizer_maximises_utility(twin):
+    a = _arr(regularizer=0.0)
+    r = twin.solve(a)
+    P = to_oracle(a)
+    best, _ = mr.brute_force_p1(P) if a.N * a.T <= 16 else (None, None)
+    got = mr.evaluate_counts(P, r["planned_rounds"])[0]
+    assert got >= best - 1e-9 * abs(best)
+
+
+def test_finished_job_and_zero_priority(twin):
+    a = _arr(completed_epochs=[10, 1], priority=[0.0, 2.0], remaining_runtime=[1.0, 150.0])
+    r = twin.solve(a)
+    check_plan_valid(a, r)
+
+
+@pytest.mark.parametrize("bad", [
+    dict(nworkers=[0, 1]), dict(total_epochs=[0, 4]), dict(completed_epochs=[11, 1]),
+    dict(epoch_duration=[0.0, 1.0]), dict(priority=[-1.0, 1.0]),
+    dict(priority=[float("nan"), 1.0]), dict(regularizer=-1.0), dict(future_rounds=65),
+])
+def test_invalid_inputs_rejected(bad, twin):
+    a = _arr(**bad)
+    assert twin.rc(a) == sn.SW_ERR_INVALID
