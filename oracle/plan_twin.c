@@ -44,9 +44,13 @@ typedef struct {
 
 #define K_(P, j, n) ((P)->key[(size_t)(j) * (P)->T + (n)])
 
-/* Deterministic sum: SW_DET_LANES contiguous chunks, then a halving tree. */
+/* Deterministic sum: SW_DET_LANES contiguous chunks summed
+ * left to right; then, per wave of 64 lanes, a halving tree p[i] += p[i+h]
+ * (h = 32 … 1); then the SW_DET_LANES/64 wave sums by the same halving tree.
+ * The GPU does exactly this with wave shuffles and one LDS exchange. */
 static double sw_detsum(const double* v, int32_t N) {
     double part[SW_DET_LANES];
+    double wsum[SW_DET_LANES / 64];
     int32_t q = (N + SW_DET_LANES - 1) / SW_DET_LANES;
     for (int32_t lane = 0; lane < SW_DET_LANES; ++lane) {
         double s = 0.0;
@@ -54,9 +58,15 @@ static double sw_detsum(const double* v, int32_t N) {
         for (int32_t j = lo; j < hi; ++j) s = s + v[j];
         part[lane] = s;
     }
-    for (int32_t h = SW_DET_LANES / 2; h >= 1; h >>= 1)
-        for (int32_t i = 0; i < h; ++i) part[i] = part[i] + part[i + h];
-    return part[0];
+    for (int32_t w = 0; w < SW_DET_LANES / 64; ++w) {
+        double* p = part + 64 * w;
+        for (int32_t h = 32; h >= 1; h >>= 1)
+            for (int32_t i = 0; i < h; ++i) p[i] = p[i] + p[i + h];
+        wsum[w] = p[0];
+    }
+    for (int32_t h = SW_DET_LANES / 128; h >= 1; h >>= 1)
+        for (int32_t i = 0; i < h; ++i) wsum[i] = wsum[i] + wsum[i + h];
+    return wsum[0];
 }
 
 static double fval(const twin_t* P, int32_t j, int32_t n) {

@@ -94,6 +94,7 @@ struct sw_handle {
     DevBuf<float> d_ws_keys;
     DevBuf<sw_jobc> d_ws_jc;
     DevBuf<sw_out_dev> d_out;
+    DevBuf<uint64_t> d_stamps; /* SW_STAMPS diagnostic builds */
     /* pinned staging */
     HostBuf<int32_t> h_w, h_F, h_E, h_planned;
     HostBuf<double> h_d, h_R, h_p;
@@ -208,7 +209,7 @@ void sw_destroy(sw_handle* h) {
     h->d_inst.release(); h->d_w.release(); h->d_F.release(); h->d_E.release();
     h->d_planned.release(); h->d_d.release(); h->d_R.release(); h->d_p.release();
     h->d_plan.release(); h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
-    h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_out.release();
+    h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_out.release(); h->d_stamps.release();
     h->h_w.release(); h->h_F.release(); h->h_E.release(); h->h_planned.release();
     h->h_d.release(); h->h_R.release(); h->h_p.release(); h->h_plan.release(); h->h_out.release();
     for (hipEvent_t ev : h->ev_pool)
@@ -246,7 +247,7 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS) {
         const int KT = maxT <= 32 ? 32 : 64;
-        if (h->d_ws_u8.reserve(Jz * SW_WS_U8) || h->d_ws_u64.reserve(Jz * 4) ||
+        if (h->d_ws_u8.reserve(Jz * SW_WS_U8) || h->d_ws_u64.reserve(Jz * SW_WS_U64) ||
             h->d_ws_sort.reserve(Jz * 4) || h->d_ws_keys.reserve(Jz * KT) ||
             h->d_ws_jc.reserve(Jz))
             return fail(h, SW_ERR_HIP, "workspace allocation failed");
@@ -309,8 +310,23 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         }
         SW_HIP(h, hipStreamSynchronize(s));
     }
+#ifdef SW_STAMPS
+    if (h->d_stamps.reserve((size_t)std::max(count, 1) * 8))
+        return fail(h, SW_ERR_HIP, "stamp buffer allocation failed");
+    SW_HIP(h, hipMemset(h->d_stamps.p, 0, (size_t)std::max(count, 1) * 8 * sizeof(uint64_t)));
+#endif
     return SW_OK;
 }
+
+#ifdef SW_STAMPS
+/* Diagnostic builds only (not part of include/shockwave_amd.h). */
+int sw_debug_stamps(sw_handle* h, uint64_t* out) {
+    SW_HIP(h, hipStreamSynchronize(h->stream));
+    SW_HIP(h, hipMemcpy(out, h->d_stamps.p, (size_t)h->count * 8 * sizeof(uint64_t),
+                        hipMemcpyDeviceToHost));
+    return SW_OK;
+}
+#endif
 
 int sw_batch_run(sw_handle* h) {
     if (!h) return SW_ERR_INVALID;
@@ -330,6 +346,9 @@ int sw_batch_run(sw_handle* h) {
     B.plan = h->d_plan.p;
     B.planned = h->d_planned.p;
     B.out = h->d_out.p;
+#ifdef SW_STAMPS
+    B.stamps = h->d_stamps.p;
+#endif
     const int one = h->maxN <= SW_LDS_JOBS;
     if (!one) {
         B.ws.u8 = h->d_ws_u8.p;

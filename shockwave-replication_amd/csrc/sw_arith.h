@@ -36,7 +36,7 @@
 /* Deterministic-reduction width: jobs are split into SW_DET_LANES contiguous
  * chunks, each summed left to right, then combined by a halving tree.  The
  * plan kernel runs exactly this many threads per instance. */
-#define SW_DET_LANES 1024
+#define SW_DET_LANES 512
 /* fp32 +inf bits: upper end of the price (key) bisection. */
 #define SW_KEY_INF_BITS 0x7F800000u
 #define SW_FLT_MIN 1.1754943508222875e-38

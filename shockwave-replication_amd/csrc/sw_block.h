@@ -1,152 +1,218 @@
 /*
- * sw_block.h — workgroup primitives for the plan kernel (1024 threads =
- * 16 wave64 wavefronts per instance).  Wave-level steps use cross-lane
- * shuffles (ds_swizzle / DPP under the hood), the cross-wave step goes through
- * LDS.  Every reduction whose result feeds a decision is exact (integers,
- * max, lexicographic max) or follows the fixed halving tree of sw_detsum, so
- * the result does not depend on wave scheduling.
+ * sw_block.h — workgroup and wavefront primitives for the plan kernel
+ * (512 threads = 8 wave64 per instance).
+ *
+ * Block reductions take ONE barrier: each wave reduces with cross-lane
+ * shuffles (DPP / ds_swizzle under the hood), lane 0 publishes its partial
+ * to an LDS slot, one __syncthreads, every thread combines the 16 partials.
+ * Successive reductions alternate between two slot sets, so no second
+ * barrier is needed before a slot is rewritten.  Every reduction whose
+ * result feeds a decision is exact (integers, max, lexicographic max) or
+ * the fixed-order tree of sw_detsum (oracle/plan_twin.c), so results do not
+ * depend on wave scheduling.
  */
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define SW_BLOCK 1024
+#define SW_BLOCK 512
 #define SW_WAVES (SW_BLOCK / 64)
 
-struct sw_scratch {
-    double dtree[SW_BLOCK];       /* halving-tree scratch (8 KB)            */
-    int64_t wsum[SW_WAVES][2];    /* per-wave partials                        */
-    uint64_t wmax[SW_WAVES];
-    double wdmax[SW_WAVES];
-    int32_t wscan[SW_WAVES];
-    int64_t bcast_i[4];
-    double bcast_d[4];
+struct sw_xchg {
+    int64_t i[2][SW_WAVES][2];
+    double d[2][SW_WAVES][2];
+    uint64_t u[2][SW_WAVES];
+    int32_t s[2][SW_WAVES];
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
+/* Order LDS accesses of one wave (the hardware keeps a wave's LDS ops in
+ * order; this keeps the compiler from moving them). */
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-        uint64_t x = __shfl_xor(v, o, 64);
+        T x = __shfl_xor(v, o, 64);
         v = x > v ? x : v;
     }
     return v;
 }
 
-__device__ __forceinline__ double wave_max_d(double v) {
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-        double x = __shfl_xor(v, o, 64);
-        v = x > v ? x : v;
+        T x = __shfl_xor(v, o, 64);
+        v = x < v ? x : v;
     }
     return v;
 }
 
-/* Sum of two int64 values over the block (one pair of barriers). */
-__device__ __forceinline__ void block_sum2(int64_t a, int64_t b, int64_t* ra, int64_t* rb,
-                                           sw_scratch* s) {
-    a = wave_sum_i64(a);
-    b = wave_sum_i64(b);
-    if (lane_id() == 0) { s->wsum[wave_id()][0] = a; s->wsum[wave_id()][1] = b; }
-    __syncthreads();
-    int64_t ta = 0, tb = 0;
-#pragma unroll
-    for (int i = 0; i < SW_WAVES; ++i) { ta += s->wsum[i][0]; tb += s->wsum[i][1]; }
-    __syncthreads();
-    *ra = ta;
-    *rb = tb;
-}
-
-__device__ __forceinline__ int64_t block_sum(int64_t a, sw_scratch* s) {
-    int64_t ra, rb;
-    block_sum2(a, 0, &ra, &rb, s);
-    return ra;
-}
-
-__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, sw_scratch* s) {
-    v = wave_max_u64(v);
-    if (lane_id() == 0) s->wmax[wave_id()] = v;
-    __syncthreads();
-    uint64_t m = 0;
-#pragma unroll
-    for (int i = 0; i < SW_WAVES; ++i) m = s->wmax[i] > m ? s->wmax[i] : m;
-    __syncthreads();
-    return m;
-}
-
-__device__ __forceinline__ double block_max_d(double v, sw_scratch* s) {
-    v = wave_max_d(v);
-    if (lane_id() == 0) s->wdmax[wave_id()] = v;
-    __syncthreads();
-    double m = s->wdmax[0];
-#pragma unroll
-    for (int i = 1; i < SW_WAVES; ++i) m = s->wdmax[i] > m ? s->wdmax[i] : m;
-    __syncthreads();
-    return m;
-}
-
-/* Exclusive prefix sum over thread order (int32).  *total gets the sum. */
-__device__ __forceinline__ int32_t block_exscan_i32(int32_t v, int32_t* total, sw_scratch* s) {
-    int lane = lane_id();
-    int32_t x = v;
+/* Inclusive prefix sum over lanes. */
+template <typename T>
+__device__ __forceinline__ T wave_incscan(T v) {
+    const int lane = lane_id();
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        int32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+        T y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
     }
-    if (lane == 63) s->wscan[wave_id()] = x;
-    __syncthreads();
-    int32_t base = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < SW_WAVES; ++i) {
-        int32_t t = s->wscan[i];
-        base += (i < wave_id()) ? t : 0;
-        tot += t;
-    }
-    __syncthreads();
-    *total = tot;
-    return base + x - v;
+    return v;
 }
 
-/*
- * Deterministic sum (must equal sw_detsum in oracle/plan_twin.c): thread i
- * holds lane i's left-to-right partial; combine p[i] += p[i+h] for
- * h = 512 … 1.  h ≥ 64 through LDS, h ≤ 32 inside wave 0.
- */
-__device__ __forceinline__ double block_detsum(double v, sw_scratch* s) {
-    int tid = threadIdx.x;
-    s->dtree[tid] = v;
-    __syncthreads();
+/* Inclusive suffix sum over lanes (lane L gets Σ_{l ≥ L}). */
+template <typename T>
+__device__ __forceinline__ T wave_sufscan(T v) {
+    const int lane = lane_id();
 #pragma unroll
-    for (int h = SW_BLOCK / 2; h >= 64; h >>= 1) {
-        if (tid < h) s->dtree[tid] = s->dtree[tid] + s->dtree[tid + h];
-        __syncthreads();
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_down(v, o, 64);
+        if (lane + o < 64) v += y;
     }
-    if (tid < 64) {
-        double x = s->dtree[tid];
-#pragma unroll
-        for (int h = 32; h >= 1; h >>= 1) {
-            double y = __shfl_down(x, h, 64);
-            x = x + y;
-        }
-        if (tid == 0) s->bcast_d[0] = x;
-    }
-    __syncthreads();
-    double r = s->bcast_d[0];
-    __syncthreads();
-    return r;
+    return v;
 }
+
+/* Fixed halving tree over the wave (p[i] += p[i+h], h = 32 … 1); the result
+ * is valid in lane 0. */
+__device__ __forceinline__ double wave_dettree(double x) {
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) {
+        double y = __shfl_down(x, h, 64);
+        x = x + y;
+    }
+    return x;
+}
+
+struct sw_blk {
+    sw_xchg* X;
+    int par;
+
+    __device__ __forceinline__ void flip() { par ^= 1; }
+
+    __device__ __forceinline__ int32_t sum32(int32_t v) {
+        v = wave_sum(v);
+        if (lane_id() == 0) X->s[par][wave_id()] = v;
+        __syncthreads();
+        int32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) t += X->s[par][w];
+        flip();
+        return t;
+    }
+
+    __device__ __forceinline__ int32_t min32(int32_t v) {
+        v = wave_min(v);
+        if (lane_id() == 0) X->s[par][wave_id()] = v;
+        __syncthreads();
+        int32_t t = X->s[par][0];
+#pragma unroll
+        for (int w = 1; w < SW_WAVES; ++w) t = X->s[par][w] < t ? X->s[par][w] : t;
+        flip();
+        return t;
+    }
+
+    __device__ __forceinline__ int64_t sum(int64_t v) {
+        v = wave_sum(v);
+        if (lane_id() == 0) X->i[par][wave_id()][0] = v;
+        __syncthreads();
+        int64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) t += X->i[par][w][0];
+        flip();
+        return t;
+    }
+
+    __device__ __forceinline__ void sum2(int64_t a, int64_t b, int64_t& ra, int64_t& rb) {
+        a = wave_sum(a);
+        b = wave_sum(b);
+        if (lane_id() == 0) { X->i[par][wave_id()][0] = a; X->i[par][wave_id()][1] = b; }
+        __syncthreads();
+        int64_t ta = 0, tb = 0;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) { ta += X->i[par][w][0]; tb += X->i[par][w][1]; }
+        flip();
+        ra = ta;
+        rb = tb;
+    }
+
+    __device__ __forceinline__ uint64_t umax(uint64_t v) {
+        v = wave_max(v);
+        if (lane_id() == 0) X->u[par][wave_id()] = v;
+        __syncthreads();
+        uint64_t m = 0;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) m = X->u[par][w] > m ? X->u[par][w] : m;
+        flip();
+        return m;
+    }
+
+    __device__ __forceinline__ double dmax(double v) {
+        v = wave_max(v);
+        if (lane_id() == 0) X->d[par][wave_id()][0] = v;
+        __syncthreads();
+        double m = X->d[par][0][0];
+#pragma unroll
+        for (int w = 1; w < SW_WAVES; ++w) m = X->d[par][w][0] > m ? X->d[par][w][0] : m;
+        flip();
+        return m;
+    }
+
+    /* sw_detsum of the per-thread partials v, and the max of m, together. */
+    __device__ __forceinline__ void detsum_max(double v, double m, double& S, double& M) {
+        v = wave_dettree(v);
+        m = wave_max(m);
+        if (lane_id() == 0) { X->d[par][wave_id()][0] = v; X->d[par][wave_id()][1] = m; }
+        __syncthreads();
+        double s[SW_WAVES];
+        double mm = X->d[par][0][1];
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) {
+            s[w] = X->d[par][w][0];
+            mm = X->d[par][w][1] > mm ? X->d[par][w][1] : mm;
+        }
+#pragma unroll
+        for (int h = SW_WAVES / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int i = 0; i < h; ++i) s[i] = s[i] + s[i + h];
+        flip();
+        S = s[0];
+        M = mm;
+    }
+
+    __device__ __forceinline__ double detsum(double v) {
+        double S, M;
+        detsum_max(v, 0.0, S, M);
+        return S;
+    }
+
+    /* Exclusive prefix sum over thread order; also returns the total. */
+    __device__ __forceinline__ int32_t exscan(int32_t v, int32_t& total) {
+        int32_t x = wave_incscan(v);
+        if (lane_id() == 63) X->s[par][wave_id()] = x;
+        __syncthreads();
+        int32_t base = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) {
+            int32_t t = X->s[par][w];
+            base += (w < wave_id()) ? t : 0;
+            tot += t;
+        }
+        flip();
+        total = tot;
+        return base + x - v;
+    }
+};

@@ -17,7 +17,7 @@
 
 #include "sw_arith.h"
 
-#define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip */
+#define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip (2 per thread) */
 
 struct sw_inst_dev {
     int32_t N, T, G, nb;
@@ -36,12 +36,13 @@ struct sw_out_dev {
 /* Global workspace, per job (used only when N > SW_LDS_JOBS). */
 struct sw_ws_dev {
     uint8_t* u8;    /* [total_jobs][SW_WS_U8]      */
-    uint64_t* u64;  /* [total_jobs][3] masks        */
+    uint64_t* u64;  /* [total_jobs][SW_WS_U64]     */
     uint64_t* sort; /* [2·total_jobs][2] sort keys  */
     float* keys;    /* [total_jobs][KT]             */
     sw_jobc* jc;    /* [total_jobs]                 */
 };
-#define SW_WS_U8 12
+#define SW_WS_U8 8   /* per-job u8 state arrays   */
+#define SW_WS_U64 6  /* per-job u64 arrays        */
 
 struct sw_batch_dev {
     const sw_inst_dev* inst;
@@ -57,4 +58,5 @@ struct sw_batch_dev {
     int32_t* planned;
     sw_out_dev* out;
     sw_ws_dev ws;
+    uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][8] cycles */
 };

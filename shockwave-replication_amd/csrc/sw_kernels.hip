@@ -2,23 +2,28 @@
  * sw_kernels.hip — the MI355X (gfx950) plan-solve kernel.
  *
  * One 1024-thread workgroup (16 wave64) solves one instance end to end:
- *   setup     per-job constants, fp32 ranking-key rows (the fused
- *             log-utility-gradient × fairness-weight step), A = max_j a_j
+ *   setup     per-job constants and fp32 ranking-key rows — the fused
+ *             log-utility-gradient × fairness-weight step — and A = max_j a_j
  *   P1        level search over the makespan M; at each level a price
- *             bisection over the fp32 key bits (the Fisher-market price of a
- *             GPU-round), a job-ordered tie group and a width tail;
- *             then packing into rounds, re-solved on a smaller budget when
- *             widths fragment rounds                        (shockwave.py:330-388)
+ *             bisection over the fp32 key bits (the price of a GPU-round),
+ *             a job-ordered tie group and a width tail; then packing into
+ *             rounds, re-solved on a smaller budget when widths fragment
+ *             the rounds                                  (shockwave.py:330-388)
  *   P2        priority placement of the planned rounds    (shockwave.py:281-328)
  *   emit      plan bytes, planned-round counts, objective  (shockwave.py:390-398)
- * The algorithm is specified by, and bit-identical to, oracle/plan_twin.c:
- * each function below names the twin function it mirrors.  DESIGN.md §3
- * describes it; §4 gives the layout and the roofline.
+ * The algorithm is specified by, and bit-identical to, oracle/plan_twin.c;
+ * functions below name the twin function they mirror.  DESIGN.md §3
+ * describes the algorithm, §4 the mapping onto CDNA4.
  *
- * Instances with N ≤ 1024 (every reference configuration: 50–900 jobs) keep
- * their whole state on chip: the job's key row in VGPRs (one job per
- * thread), everything else in LDS.  Larger instances (the 10k-job C4 shape)
- * keep per-job state in an HBM workspace (L2-resident) instead.
+ * Mapping.  N ≤ 1024 (every reference configuration): one job per thread,
+ * the job's fp32 key row in VGPRs, per-job state in LDS, every block
+ * reduction one barrier (sw_block.h).  Packing sorts the jobs with a
+ * register bitonic sort (shuffles for strides < 64, LDS beyond), then ONE
+ * wavefront runs the sequential round loop with wave-level scans and ballots
+ * over LDS-resident position state — no block barriers inside the loop.
+ * N > 1024 (the 10k-job C4 shape): several jobs per thread, per-job state
+ * and key rows in an HBM workspace (L2-resident), sort through the
+ * workspace.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,15 +35,33 @@
 
 namespace {
 
+#ifdef SW_STAMPS
+#define SW_STAMP(slot)                                                            \
+    do {                                                                          \
+        __syncthreads();                                                          \
+        if (threadIdx.x == 0 && B.stamps) {                                       \
+            uint64_t now_ = __builtin_amdgcn_s_memtime();                         \
+            B.stamps[(size_t)blockIdx.x * 8 + (slot)] += now_ - stamp_prev_;      \
+            stamp_prev_ = now_;                                                   \
+        }                                                                         \
+    } while (0)
+#else
+#define SW_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+
 struct SelEval {
     double U, Mact, J, ubound;
 };
 
-__device__ __forceinline__ uint32_t next_pow2(uint32_t v) {
-    uint32_t p = 1;
-    while (p < v) p <<= 1;
-    return p;
-}
+/* packed per-position packer state: r | w << 8 | sel << 16 */
+__device__ __forceinline__ uint32_t st_r(uint32_t s) { return s & 0xFFu; }
+__device__ __forceinline__ uint32_t st_w(uint32_t s) { return (s >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t st_sel(uint32_t s) { return (s >> 16) & 1u; }
+
+/* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = 2 · SW_BLOCK) */
+#define SW_JPT 2
 
 template <int KT, bool ONE>
 struct Ctx {
@@ -50,25 +73,24 @@ struct Ctx {
     const sw_inst_dev* inst;
     const double* beta; /* LDS */
     const double* ell;  /* LDS */
-    sw_scratch* S;
+    sw_blk blk;
     /* inputs (instance-relative) */
     const int32_t* w_in;
     const double* p_in;
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
     uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
-    /* per-position state of the packer */
-    uint8_t *rpos, *wpos, *selp;
-    int32_t* ordj;
     uint64_t *ycur, *ybest, *y2;
-    uint64_t *shi, *slo;
-    /* small LDS arrays */
+    /* packer: transposed position state, masks, order, sort buffers */
+    uint32_t* pst;
+    uint64_t* pmask;
+    int32_t* pord;
+    uint64_t* sbuf; /* ONE: [2][2][1024] bitonic exchange; else [2][NP] keys */
     int32_t *H, *SH;
-    int64_t* need;
     int64_t* misc;
-    /* this thread's job (ONE) */
-    sw_jobc jc0;
-    float kr[KT];
-    /* global per-job data (!ONE) */
+    /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
+    sw_jobc jcs[SW_JPT];
+    float kr[SW_JPT][KT];
+    /* per-job data in HBM (!ONE) */
     float* gkeys;
     sw_jobc* gjc;
 
@@ -77,60 +99,97 @@ struct Ctx {
         int h = jlo() + q;
         return h < N ? h : N;
     }
-    __device__ __forceinline__ const sw_jobc& jc(int j) const {
+    /* Visit this thread's jobs in order; s is a compile-time slot on the
+     * on-chip path, 0 otherwise. */
+    template <class F>
+    __device__ __forceinline__ void for_jobs(F&& f) const {
+        if constexpr (ONE) {
+#pragma unroll
+            for (int s = 0; s < SW_JPT; ++s) {
+                const int j = jlo() + s;
+                if (s < q && j < N) f(j, s);
+            }
+        } else {
+            for (int j = jlo(); j < jhi(); ++j) f(j, 0);
+        }
+    }
+    __device__ __forceinline__ const sw_jobc& jc(int j, int s) const {
         if constexpr (ONE) {
             (void)j;
-            return jc0;
+            return jcs[s];
         } else {
+            (void)s;
             return gjc[j];
         }
     }
-    __device__ __forceinline__ int Tj(int j) const { return jc(j).w <= G ? T : 0; }
-    __device__ __forceinline__ double fval(int j, int n) const {
-        return sw_f(&jc(j), n, nb, beta, ell);
+    __device__ __forceinline__ int Tj(int j, int s) const { return jc(j, s).w <= G ? T : 0; }
+    __device__ __forceinline__ double fval(int j, int s, int n) const {
+        return sw_f(&jc(j, s), n, nb, beta, ell);
     }
-    __device__ __forceinline__ double gval(int j, int n) const { return sw_g(&jc(j), n); }
+    __device__ __forceinline__ double gval(int j, int s, int n) const {
+        return sw_g(&jc(j, s), n);
+    }
 
-    __device__ __forceinline__ uint32_t kbits(int j, int n) const {
+    __device__ __forceinline__ uint32_t kbits(int j, int s, int n) const {
         if constexpr (ONE) {
             (void)j;
             uint32_t v = 0;
 #pragma unroll
-            for (int i = 0; i < KT; ++i) v = (i == n) ? sw_fbits_of(kr[i]) : v;
+            for (int i = 0; i < KT; ++i) v = (i == n) ? sw_fbits_of(kr[s][i]) : v;
             return v;
         } else {
+            (void)s;
             return sw_fbits_of(gkeys[(size_t)j * KT + n]);
         }
     }
-    /* twin: lforce */
-    __device__ __forceinline__ int lforce(int j, double M) const {
-        const sw_jobc& c = jc(j);
-        int tj = Tj(j), cnt = 0;
-        if constexpr (ONE) {
-#pragma unroll
-            for (int n = 0; n < KT; ++n) cnt += (n < tj && sw_g(&c, n) > M);
-        } else {
-            for (int n = 0; n < tj; ++n) cnt += (sw_g(&c, n) > M);
+
+    /* #{n ∈ [0, hi) : g(n) > x} for the nonincreasing g — the first n with
+     * g(n) ≤ x, by binary search (twin: the counting loops). */
+    __device__ __forceinline__ int g_count_gt(const sw_jobc& c, int hi, double x) const {
+        int lo = 0;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sw_g(&c, mid) > x) lo = mid + 1; else hi = mid;
         }
-        return cnt;
+        return lo;
     }
-    /* twin: cnt_gt / cnt_ge */
+    __device__ __forceinline__ int g_count_ge(const sw_jobc& c, int hi, double x) const {
+        int lo = 0;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sw_g(&c, mid) >= x) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    }
+    /* twin: lforce */
+    __device__ __forceinline__ int lforce(int j, int s, double M) const {
+        return g_count_gt(jc(j, s), Tj(j, s), M);
+    }
+    /* twin: cnt_gt / cnt_ge.  Keys are nonincreasing, so the items with
+     * key > ρ (≥ ρ) form a prefix [0, c) and the count over [l, Tj) is
+     * min(c, Tj) − l, clamped at 0.  On chip the register row is zero past
+     * Tj, so c needs one compare per key. */
     template <bool GE>
-    __device__ __forceinline__ int cnt(int j, uint32_t rho, int l) const {
-        int tj = Tj(j), c = 0;
+    __device__ __forceinline__ int cnt(int j, int s, uint32_t rho, int l) const {
+        const int tj = Tj(j, s);
+        int c = 0;
         if constexpr (ONE) {
 #pragma unroll
             for (int n = 0; n < KT; ++n) {
-                uint32_t b = sw_fbits_of(kr[n]);
-                bool hit = GE ? (b >= rho) : (b > rho);
-                c += (n >= l && n < tj && hit);
+                const uint32_t b = sw_fbits_of(kr[s][n]);
+                c += (GE ? (b >= rho) : (b > rho)) ? 1 : 0;
             }
+            c = (c < tj ? c : tj) - l;
+            c = c > 0 ? c : 0;
         } else {
             const float* row = gkeys + (size_t)j * KT;
-            for (int n = l; n < tj; ++n) {
-                uint32_t b = sw_fbits_of(row[n]);
-                c += GE ? (b >= rho) : (b > rho);
+            int lo = l, hi = tj;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const uint32_t b = sw_fbits_of(row[mid]);
+                if (GE ? (b >= rho) : (b > rho)) lo = mid + 1; else hi = mid;
             }
+            c = lo - l;
         }
         return c;
     }
@@ -138,29 +197,51 @@ struct Ctx {
     /* twin: build() — constants and key rows */
     __device__ __forceinline__ void setup() {
         double amax = 0.0;
-        for (int j = jlo(); j < jhi(); ++j) amax = sw_max(amax, jc(j).a);
-        A = block_max_d(amax, S);
-        for (int j = jlo(); j < jhi(); ++j) {
-            const sw_jobc& c = jc(j);
-            double prev = sw_f(&c, 0, nb, beta, ell), vm = 0.0;
-            if constexpr (ONE) {
+        for_jobs([&](int j, int s) { amax = sw_max(amax, jc(j, s).a); });
+        A = blk.dmax(amax);
+        if constexpr (ONE) {
+            /* rolled evaluation into an LDS staging window (8 keys × 2 jobs
+             * per thread per chunk), then compile-time-indexed copies */
+            float* stage = reinterpret_cast<float*>(sbuf);
+            double prev[SW_JPT], vm[SW_JPT];
 #pragma unroll
-                for (int n = 0; n < KT; ++n) {
-                    float kv = 0.0f;
-                    if (n < T) {
-                        double cur = sw_f(&c, n + 1, nb, beta, ell);
-                        double v = sw_pos(cur - prev);
-                        vm = (n == 0) ? v : sw_min(vm, v);
-                        kv = sw_key(vm, c.w, A);
-                        prev = cur;
+            for (int s = 0; s < SW_JPT; ++s) {
+                prev[s] = 0.0;
+                vm[s] = 0.0;
+                if (s < q && jlo() + s < N) prev[s] = sw_f(&jcs[s], 0, nb, beta, ell);
+            }
+#pragma unroll
+            for (int ch = 0; ch < KT / 8; ++ch) {
+#pragma unroll
+                for (int s = 0; s < SW_JPT; ++s) {
+                    const bool act = s < q && jlo() + s < N;
+                    for (int i = 0; i < 8; ++i) {
+                        const int n = ch * 8 + i;
+                        float kv = 0.0f;
+                        if (act && n < T && jcs[s].w <= G) {
+                            const double cur = sw_f(&jcs[s], n + 1, nb, beta, ell);
+                            const double v = sw_pos(cur - prev[s]);
+                            vm[s] = (n == 0) ? v : sw_min(vm[s], v);
+                            kv = sw_key(vm[s], jcs[s].w, A);
+                            prev[s] = cur;
+                        }
+                        stage[(s * 8 + i) * SW_BLOCK + threadIdx.x] = kv;
                     }
-                    kr[n] = kv;
                 }
-            } else {
+#pragma unroll
+                for (int s = 0; s < SW_JPT; ++s)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        kr[s][ch * 8 + i] = stage[(s * 8 + i) * SW_BLOCK + threadIdx.x];
+            }
+        } else {
+            for (int j = jlo(); j < jhi(); ++j) {
+                const sw_jobc& c = gjc[j];
+                double prev = sw_f(&c, 0, nb, beta, ell), vm = 0.0;
                 float* row = gkeys + (size_t)j * KT;
                 for (int n = 0; n < T; ++n) {
-                    double cur = sw_f(&c, n + 1, nb, beta, ell);
-                    double v = sw_pos(cur - prev);
+                    const double cur = sw_f(&c, n + 1, nb, beta, ell);
+                    const double v = sw_pos(cur - prev);
                     vm = (n == 0) ? v : sw_min(vm, v);
                     row[n] = sw_key(vm, c.w, A);
                     prev = cur;
@@ -173,61 +254,59 @@ struct Ctx {
     /* twin: select_level */
     __device__ __forceinline__ SelEval select_level(double M, bool is_inf) {
         int64_t wf = 0, wall = 0;
-        for (int j = jlo(); j < jhi(); ++j) {
-            int l = is_inf ? 0 : lforce(j, M);
+        for_jobs([&](int j, int s) {
+            const int l = is_inf ? 0 : lforce(j, s, M);
             lcur[j] = (uint8_t)l;
-            wf += (int64_t)jc(j).w * l;
-            wall += (int64_t)jc(j).w * (Tj(j) - l);
-        }
+            wf += (int64_t)jc(j, s).w * l;
+            wall += (int64_t)jc(j, s).w * (Tj(j, s) - l);
+        });
         int64_t Wf, Wall;
-        block_sum2(wf, wall, &Wf, &Wall, S);
+        blk.sum2(wf, wall, Wf, Wall);
         passes++;
         SelEval ev;
         if (Wf > C) {
             ev.U = 0; ev.Mact = 0; ev.J = -1e308; ev.ubound = 0;
             return ev;
         }
-        int64_t bud = C - Wf;
+        const int64_t bud = C - Wf;
         double rho_d = 0.0;
         int64_t wgt_star;
         if (Wall <= bud) {
-            for (int j = jlo(); j < jhi(); ++j) {
-                ncur[j] = (uint8_t)Tj(j);
-                tkcur[j] = (uint8_t)(Tj(j) - lcur[j]);
-            }
+            for_jobs([&](int j, int s) {
+                ncur[j] = (uint8_t)Tj(j, s);
+                tkcur[j] = (uint8_t)(Tj(j, s) - lcur[j]);
+            });
             wgt_star = Wall;
         } else {
             uint32_t lo = 0, hi = SW_KEY_INF_BITS;
             while (lo < hi) {
-                uint32_t mid = lo + ((hi - lo) >> 1);
-                int64_t wg = 0;
-                for (int j = jlo(); j < jhi(); ++j)
-                    wg += (int64_t)jc(j).w * cnt<false>(j, mid, lcur[j]);
-                wg = block_sum(wg, S);
+                const uint32_t mid = lo + ((hi - lo) >> 1);
+                int32_t wg = 0;
+                for_jobs([&](int j, int s) { wg += jc(j, s).w * cnt<false>(j, s, mid, lcur[j]); });
+                wg = blk.sum32(wg);
                 passes++;
                 if (wg <= bud) hi = mid; else lo = mid + 1;
             }
             const uint32_t rho = lo;
             rho_d = (double)sw_float_of(rho);
             int64_t wt_l = 0;
-            int32_t tie_w_l = 0;
-            for (int j = jlo(); j < jhi(); ++j) {
-                int tk = cnt<false>(j, rho, lcur[j]);
+            int32_t tie_l = 0;
+            for_jobs([&](int j, int s) {
+                const int tk = cnt<false>(j, s, rho, lcur[j]);
                 tkcur[j] = (uint8_t)tk;
-                wt_l += (int64_t)jc(j).w * tk;
-                int tie = cnt<true>(j, rho, lcur[j]) - tk;
-                tie_w_l += jc(j).w * tie;
-            }
-            const int64_t wt = block_sum(wt_l, S);
+                wt_l += (int64_t)jc(j, s).w * tk;
+                tie_l += jc(j, s).w * (cnt<true>(j, s, rho, lcur[j]) - tk);
+            });
+            const int64_t wt = blk.sum(wt_l);
             wgt_star = wt;
             const int64_t rem = bud - wt;
             int32_t tot;
-            int64_t excl = block_exscan_i32(tie_w_l, &tot, S);
+            int64_t excl = blk.exscan(tie_l, tot);
             int64_t used_l = 0;
-            for (int j = jlo(); j < jhi(); ++j) {
+            for_jobs([&](int j, int s) {
                 const int tk = tkcur[j];
-                const int tie = cnt<true>(j, rho, lcur[j]) - tk;
-                const int64_t wj = jc(j).w;
+                const int tie = cnt<true>(j, s, rho, lcur[j]) - tk;
+                const int64_t wj = jc(j, s).w;
                 int tt;
                 if (excl + wj * tie <= rem) tt = tie;
                 else if (excl <= rem) tt = (int)((rem - excl) / wj);
@@ -235,20 +314,21 @@ struct Ctx {
                 ncur[j] = (uint8_t)(lcur[j] + tk + tt);
                 used_l += wj * tt;
                 excl += wj * tie;
-            }
-            const int64_t used = block_sum(used_l, S);
+            });
+            const int64_t used = blk.sum(used_l);
             passes++;
             int64_t rem2 = rem - used;
             while (rem2 > 0) {
                 uint64_t best = 0;
-                for (int j = jlo(); j < jhi(); ++j) {
-                    int nj = ncur[j];
-                    if (nj < Tj(j) && (int64_t)jc(j).w <= rem2) {
-                        uint64_t key = ((uint64_t)kbits(j, nj) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)j);
+                for_jobs([&](int j, int s) {
+                    const int nj = ncur[j];
+                    if (nj < Tj(j, s) && (int64_t)jc(j, s).w <= rem2) {
+                        const uint64_t key = ((uint64_t)kbits(j, s, nj) << 32) |
+                                             (uint64_t)(0xFFFFFFFFu - (uint32_t)j);
                         best = key > best ? key : best;
                     }
-                }
-                best = block_max_u64(best, S);
+                });
+                best = blk.umax(best);
                 passes++;
                 if (best == 0) break;
                 const int jb = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu));
@@ -256,17 +336,15 @@ struct Ctx {
                 rem2 -= w_in[jb];
             }
         }
-        double fs = 0.0, gm = 0.0;
-        for (int j = jlo(); j < jhi(); ++j) {
-            fs = fs + fval(j, ncur[j]);
-            gm = sw_max(gm, gval(j, ncur[j]));
-        }
-        ev.U = block_detsum(fs, S);
-        ev.Mact = block_max_d(gm, S);
+        double fs = 0.0, gm = 0.0, ub = 0.0;
+        for_jobs([&](int j, int s) {
+            fs = fs + fval(j, s, ncur[j]);
+            gm = sw_max(gm, gval(j, s, ncur[j]));
+            ub = ub + fval(j, s, lcur[j] + tkcur[j]);
+        });
+        blk.detsum_max(fs, gm, ev.U, ev.Mact);
         ev.J = ev.U - k * ev.Mact;
-        double ub = 0.0;
-        for (int j = jlo(); j < jhi(); ++j) ub = ub + fval(j, lcur[j] + tkcur[j]);
-        ev.ubound = block_detsum(ub, S) + (rho_d * A) * (double)(bud - wgt_star);
+        ev.ubound = blk.detsum(ub) + (rho_d * A) * (double)(bud - wgt_star);
         passes++;
         return ev;
     }
@@ -274,92 +352,166 @@ struct Ctx {
     __device__ __forceinline__ void keep_best(const SelEval& e, SelEval& best) {
         if (e.J > best.J || (e.J == best.J && e.Mact < best.Mact)) {
             best = e;
-            for (int j = jlo(); j < jhi(); ++j) nbest[j] = ncur[j];
+            for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
         }
     }
 
     /* twin: feasible_level */
     __device__ __forceinline__ bool feasible_level(double M) {
         int64_t wf = 0;
-        for (int j = jlo(); j < jhi(); ++j) wf += (int64_t)jc(j).w * lforce(j, M);
-        wf = block_sum(wf, S);
+        for_jobs([&](int j, int s) { wf += (int64_t)jc(j, s).w * lforce(j, s, M); });
+        wf = blk.sum(wf);
         passes++;
         return wf <= C;
     }
 
-    /* twin: levels_between */
+    /* twin: levels_between — #{(j, n ≤ Tj) : a < g_j(n) < b} */
     __device__ __forceinline__ int64_t levels_between(double a, double b) {
         int64_t c = 0;
-        for (int j = jlo(); j < jhi(); ++j) {
-            const sw_jobc& cj = jc(j);
-            int tj = Tj(j);
-            if constexpr (ONE) {
-#pragma unroll
-                for (int n = 0; n <= KT; ++n) {
-                    double v = sw_g(&cj, n);
-                    c += (n <= tj && v > a && v < b);
-                }
-            } else {
-                for (int n = 0; n <= tj; ++n) {
-                    double v = sw_g(&cj, n);
-                    c += (v > a && v < b);
-                }
-            }
-        }
-        c = block_sum(c, S);
+        for_jobs([&](int j, int s) {
+            const sw_jobc& cj = jc(j, s);
+            const int n1 = Tj(j, s) + 1;
+            const int d = g_count_gt(cj, n1, a) - g_count_ge(cj, n1, b);
+            c += d > 0 ? d : 0;
+        });
+        c = blk.sum(c);
         passes++;
         return c;
     }
 
-    /* twin: level_search — best counts land in nbest; returns the bound */
+    /* twin: level_search — best counts land in nbest; returns the bound.
+     * Written as a loop over evaluation requests so select_level has a
+     * single call site (phase 0: M = +inf; 1: M = M_lo; 2/3: golden m1/m2). */
     __device__ __forceinline__ double level_search() {
-        SelEval best = select_level(0.0, true);
-        for (int j = jlo(); j < jhi(); ++j) nbest[j] = ncur[j];
-        const double U_inf = best.U, M_free = best.Mact, ub_inf = best.ubound;
-        double M_lo = M_free;
-        if (N > 0 && k > 0.0) {
-            double lb = 0.0;
-            for (int j = jlo(); j < jhi(); ++j) lb = sw_max(lb, gval(j, Tj(j)));
-            lb = block_max_d(lb, S);
-            uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
-            while (lo < hi) {
-                uint64_t mid = lo + ((hi - lo) >> 1);
-                if (feasible_level(sw_from_bits(mid))) hi = mid; else lo = mid + 1;
+        SelEval best, e1;
+        best.U = best.Mact = best.ubound = 0.0;
+        best.J = -1e308;
+        e1 = best;
+        double U_inf = 0.0, M_free = 0.0, ub_inf = 0.0, M_lo = 0.0;
+        double a = 0.0, b = 0.0, m1 = 0.0, m2 = 0.0;
+        int phase = 0, it = 0;
+        while (true) {
+            double M = 0.0;
+            if (phase == 1) M = M_lo;
+            else if (phase == 2) M = m1;
+            else if (phase == 3) M = m2;
+            const SelEval ev = select_level(M, phase == 0);
+            if (phase == 0) {
+                best = ev;
+                for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
+                U_inf = ev.U;
+                M_free = ev.Mact;
+                ub_inf = ev.ubound;
+                M_lo = M_free;
+                if (!(N > 0 && k > 0.0)) break;
+                double lb = 0.0;
+                for_jobs([&](int j, int s) { lb = sw_max(lb, gval(j, s, Tj(j, s))); });
+                lb = blk.dmax(lb);
+                uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
+                while (lo < hi) {
+                    const uint64_t mid = lo + ((hi - lo) >> 1);
+                    if (feasible_level(sw_from_bits(mid))) hi = mid; else lo = mid + 1;
+                }
+                M_lo = sw_from_bits(lo);
+                phase = 1;
+                continue;
             }
-            M_lo = sw_from_bits(lo);
-            SelEval ev = select_level(M_lo, false);
             keep_best(ev, best);
-            const double width = (U_inf - ev.U) / k;
-            double a = M_lo, b = sw_min(M_free, M_lo + width);
-            for (int it = 0; it < SW_GS_ITERS; ++it) {
-                if (!(a < b)) break;
-                if (levels_between(a, b) == 0) break;
-                const double m1 = a + (b - a) * SW_GS_A;
-                const double m2 = a + (b - a) * SW_GS_B;
-                SelEval e1 = select_level(m1, false);
-                keep_best(e1, best);
-                SelEval e2 = select_level(m2, false);
-                keep_best(e2, best);
-                if (e1.J >= e2.J) b = m2; else a = m1;
+            if (phase == 1) {
+                const double width = (U_inf - ev.U) / k;
+                a = M_lo;
+                b = sw_min(M_free, M_lo + width);
+                it = 0;
+            } else if (phase == 2) {
+                e1 = ev;
+                phase = 3;
+                continue;
+            } else {
+                if (e1.J >= ev.J) b = m2; else a = m1;
+                ++it;
             }
+            /* next golden-section pair, if any */
+            if (it >= SW_GS_ITERS || !(a < b)) break;
+            if (levels_between(a, b) == 0) break;
+            m1 = a + (b - a) * SW_GS_A;
+            m2 = a + (b - a) * SW_GS_B;
+            phase = 2;
         }
         __syncthreads();
         return ub_inf - k * M_lo;
     }
 
-    /* Bitonic sort of (shi, slo) descending over NP entries, staged in LDS. */
-    __device__ __forceinline__ void bitonic_desc(int NP) {
+    /* ---- packing ---------------------------------------------------------- */
+
+    /* position p (of A, PPL per lane of wave 0) → transposed slot */
+    __device__ __forceinline__ int tslot(int p, int PPL) const { return (p % PPL) * 64 + p / PPL; }
+
+    /* Sort (hi, lo) descending.  ONE: register bitonic over 1024 elements,
+     * two per thread (element e = 2·tid + s).  Stride 1 compares inside the
+     * thread, strides 2 … 64 pair threads of one wave (shuffles), larger
+     * strides go through a double-buffered LDS exchange (one barrier per
+     * stage).  After the sort thread t holds positions 2t and 2t + 1. */
+    __device__ __forceinline__ void sort_regs(uint64_t (&hi)[2], uint64_t (&lo)[2]) {
+        const int tid = threadIdx.x;
+        int buf = 0;
+        for (int kk = 2; kk <= 2 * SW_BLOCK; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                if (jj == 1) {
+                    const bool up = ((2 * tid) & kk) == 0;
+                    const bool gt = (hi[0] > hi[1]) || (hi[0] == hi[1] && lo[0] > lo[1]);
+                    if (up ? !gt : gt) {
+                        const uint64_t th = hi[0], tl = lo[0];
+                        hi[0] = hi[1]; lo[0] = lo[1]; hi[1] = th; lo[1] = tl;
+                    }
+                    continue;
+                }
+                uint64_t ph[2], pl[2];
+                const int tj = jj >> 1;
+                if (tj >= 64) {
+                    uint64_t* xh = sbuf + (size_t)buf * 4 * SW_BLOCK;
+                    uint64_t* xl = xh + 2 * SW_BLOCK;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) { xh[2 * tid + s] = hi[s]; xl[2 * tid + s] = lo[s]; }
+                    __syncthreads();
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        ph[s] = xh[(2 * tid + s) ^ jj];
+                        pl[s] = xl[(2 * tid + s) ^ jj];
+                    }
+                    buf ^= 1;
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        ph[s] = __shfl_xor(hi[s], tj, 64);
+                        pl[s] = __shfl_xor(lo[s], tj, 64);
+                    }
+                }
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int e = 2 * tid + s;
+                    const bool up = (e & kk) == 0;
+                    const bool lower = (e & jj) == 0;
+                    const bool mine_gt = (hi[s] > ph[s]) || (hi[s] == ph[s] && lo[s] > pl[s]);
+                    const bool keep_max = (lower == up);
+                    if (keep_max ? !mine_gt : mine_gt) { hi[s] = ph[s]; lo[s] = pl[s]; }
+                }
+            }
+        }
+    }
+
+    /* Sort in the HBM workspace (!ONE): bitonic over NP entries. */
+    __device__ __forceinline__ void sort_global(int NP) {
+        uint64_t* shi = sbuf;
+        uint64_t* slo = sbuf + NP;
         for (int kk = 2; kk <= NP; kk <<= 1) {
             for (int jj = kk >> 1; jj > 0; jj >>= 1) {
                 for (int i = threadIdx.x; i < NP; i += SW_BLOCK) {
-                    int ixj = i ^ jj;
+                    const int ixj = i ^ jj;
                     if (ixj > i) {
-                        uint64_t ah = shi[i], al = slo[i], bh = shi[ixj], bl = slo[ixj];
-                        bool a_gt = (ah > bh) || (ah == bh && al > bl);
-                        bool up = ((i & kk) == 0);
-                        /* descending overall: in "up" blocks larger first */
-                        bool swap = up ? !a_gt : a_gt;
-                        if (swap) {
+                        const uint64_t ah = shi[i], al = slo[i], bh = shi[ixj], bl = slo[ixj];
+                        const bool a_gt = (ah > bh) || (ah == bh && al > bl);
+                        const bool up = (i & kk) == 0;
+                        if (up ? !a_gt : a_gt) {
                             shi[i] = bh; slo[i] = bl; shi[ixj] = ah; slo[ixj] = al;
                         }
                     }
@@ -369,162 +521,339 @@ struct Ctx {
         }
     }
 
+    /* Order key of job j for pack<MODE> (twin: the k1/k2 of each caller). */
+    __device__ __forceinline__ void key_of(int MODE, const uint8_t* nin, double Mb, int j, int s,
+                                           uint64_t& khi, uint64_t& klo) const {
+        const int nj = nin[j];
+        khi = 0;
+        klo = 0;
+        if (nj > 0) {
+            uint64_t k1;
+            uint32_t k2;
+            if (MODE != 2) {
+                const double lvl = gval(j, s, nj - 1);
+                const bool crit = k > 0.0 && lvl > Mb;
+                k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (MODE == 3 ? (uint64_t)jc(j, s).w : 0);
+                k2 = kbits(j, s, nj - 1);
+            } else {
+                k1 = sw_bits(p_in[j] / (double)nj);
+                k2 = 0;
+            }
+            khi = k1;
+            klo = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)j);
+        }
+    }
+
     /*
      * twin: pack — place nin[j] rounds per job into T rounds of capacity G.
-     * MODE 1: P1 packing order (makespan-critical first, then marginal key);
-     * MODE 2: P2 order (p_j / n_j desc).  Writes masks y[job], placed[job].
+     * MODE 1 / 3: P1 packing orders A / B; MODE 2: P2 order (p_j / n_j).
+     * Writes y[job] (round bitmask) and placed_out[job].
      */
-    template <int MODE>
-    __device__ __forceinline__ void pack(const uint8_t* nin, uint64_t* y, uint8_t* placed_out) {
+    __device__ __forceinline__ void pack(int MODE, const uint8_t* nin, uint64_t* y,
+                                         uint8_t* placed_out) {
         __syncthreads();
         double Mb = 0.0;
         if (MODE != 2) {
-            for (int j = jlo(); j < jhi(); ++j) Mb = sw_max(Mb, gval(j, nin[j]));
-            Mb = block_max_d(Mb, S);
+            for_jobs([&](int j, int s) { Mb = sw_max(Mb, gval(j, s, nin[j])); });
+            Mb = blk.dmax(Mb);
         }
-        const int NP = (int)next_pow2((uint32_t)(N > 0 ? N : 1));
-        for (int i = threadIdx.x; i < NP; i += SW_BLOCK) { shi[i] = 0; slo[i] = 0; }
-        __syncthreads();
-        int act_l = 0;
-        for (int j = jlo(); j < jhi(); ++j) {
-            y[j] = 0;
-            const int nj = nin[j];
-            if (nj > 0) {
-                uint64_t k1;
-                uint32_t k2;
-                if (MODE != 2) {
-                    /* twin: orders A (MODE 1) and B (MODE 3) */
-                    double lvl = gval(j, nj - 1);
-                    bool crit = k > 0.0 && lvl > Mb;
-                    k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (MODE == 3 ? (uint64_t)jc(j).w : 0);
-                    k2 = kbits(j, nj - 1);
-                } else {
-                    k1 = sw_bits(p_in[j] / (double)nj);
-                    k2 = 0;
-                }
-                shi[j] = k1;
-                slo[j] = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)j);
-                act_l++;
+        int64_t act_l = 0;
+        if constexpr (ONE) {
+            uint64_t khi[2] = {0, 0}, klo[2] = {0, 0};
+            for_jobs([&](int j, int s) {
+                key_of(MODE, nin, Mb, j, s, khi[s], klo[s]);
+                act_l += nin[j] > 0;
+                y[j] = 0;
+            });
+            const int A_ = (int)blk.sum(act_l);
+            sort_regs(khi, klo);
+            uint32_t st[2];
+            uint64_t mk[2] = {0, 0};
+            int jp[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int p = 2 * (int)threadIdx.x + s;
+                jp[s] = (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
+                st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | ((uint32_t)w_in[jp[s]] << 8)) : 0u;
             }
+            rounds_block(A_, st, mk);
+            for_jobs([&](int j, int s) { (void)s; placed_out[j] = 0; });
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int p = 2 * (int)threadIdx.x + s;
+                if (p < A_) {
+                    y[jp[s]] = mk[s];
+                    placed_out[jp[s]] = (uint8_t)(nin[jp[s]] - st_r(st[s]));
+                }
+            }
+            __syncthreads();
+        } else {
+            int NPg = 1;
+            while (NPg < N) NPg <<= 1;
+            uint64_t* shi = sbuf;
+            uint64_t* slo = sbuf + NPg;
+            for (int i = threadIdx.x; i < NPg; i += SW_BLOCK) { shi[i] = 0; slo[i] = 0; }
+            __syncthreads();
+            for (int j = jlo(); j < jhi(); ++j) {
+                uint64_t khi, klo;
+                key_of(MODE, nin, Mb, j, 0, khi, klo);
+                shi[j] = khi;
+                slo[j] = klo;
+                act_l += nin[j] > 0;
+                y[j] = 0;
+            }
+            const int A_ = (int)blk.sum(act_l);
+            sort_global(NPg);
+            const int PPL = (A_ + 63) / 64;
+            for (int p = threadIdx.x; p < A_; p += SW_BLOCK) {
+                const int j = (int)(0xFFFFFFFFu - (uint32_t)(slo[p] & 0xFFFFFFFFu));
+                const int s = tslot(p, PPL);
+                pord[s] = j;
+                pst[s] = (uint32_t)nin[j] | ((uint32_t)w_in[j] << 8);
+                pmask[s] = 0;
+            }
+            __syncthreads();
+            if (wave_id() == 0) rounds(A_, PPL);
+            __syncthreads();
+            for (int j = jlo(); j < jhi(); ++j) placed_out[j] = 0;
+            __syncthreads();
+            for (int p = threadIdx.x; p < A_; p += SW_BLOCK) {
+                const int s = tslot(p, PPL);
+                const int j = pord[s];
+                y[j] = pmask[s];
+                placed_out[j] = (uint8_t)(nin[j] - st_r(pst[s]));
+            }
+            __syncthreads();
         }
-        const int A_ = (int)block_sum(act_l, S);
-        bitonic_desc(NP);
-        const int q2 = (A_ + SW_BLOCK - 1) / SW_BLOCK;
-        const int plo = (int)threadIdx.x * q2;
-        const int phi = plo + q2 < A_ ? plo + q2 : A_;
-        for (int i = plo; i < phi; ++i) {
-            const int j = (int)(0xFFFFFFFFu - (uint32_t)(slo[i] & 0xFFFFFFFFu));
-            ordj[i] = j;
-            rpos[i] = nin[j];
-            wpos[i] = (uint8_t)w_in[j];
-            selp[i] = 0;
-        }
+    }
+
+    /* The round loop of pack, run by wave 0 alone (twin: the t loop of
+     * pack).  Lane L owns positions [L·PPL, L·PPL + PPL) (prefix order =
+     * lane-major); their state lives at tslot(p). */
+    __device__ __forceinline__ void rounds(int A_, int PPL) {
+        rounds_mem(A_, PPL);
+    }
+
+    /* ONE: all 8 waves; thread t keeps its positions 2t, 2t+1 (as left by
+     * the sort) in VGPRs.  Block scans/sums take one barrier each; the
+     * histograms H/SH are double-buffered by round parity. */
+    __device__ __forceinline__ void rounds_block(int A_, uint32_t (&st)[2], uint64_t (&mk)[2]) {
+        const int tid = threadIdx.x;
+        const int lane = lane_id();
+        int32_t* Hb[2] = {H, H + 68};
+        int32_t* SHb[2] = {SH, SH + 68};
+        if (tid < 65) { Hb[0][tid] = 0; SHb[0][tid] = 0; }
         __syncthreads();
         for (int t = 0; t < T; ++t) {
             const int R = T - t;
-            int64_t cap = G;
-            if ((int)threadIdx.x <= R) { H[threadIdx.x] = 0; SH[threadIdx.x] = 0; }
-            __syncthreads();
-            for (int i = plo; i < phi; ++i) {
-                int rr = rpos[i] < R ? rpos[i] : R;
-                atomicAdd(&H[rr], (int32_t)wpos[i]);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                int64_t S0 = 0, S1 = 0;
-                for (int m = R - 1; m >= 0; --m) {
-                    const int v = m + 1;
-                    S0 += H[v];
-                    S1 += (int64_t)v * H[v];
-                    need[m] = (S1 - (int64_t)m * S0) - (int64_t)G * (R - 1 - m);
+            int32_t* Hc = Hb[t & 1];
+            int32_t* SHc = SHb[t & 1];
+            int32_t cap = G;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (2 * tid + i < A_) {
+                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
+                    atomicAdd(&Hc[rr], (int32_t)st_w(st[i]));
                 }
             }
+            /* clear next round's buffers (read by nobody this round) */
+            if (tid < 65) { Hb[(t + 1) & 1][tid] = 0; SHb[(t + 1) & 1][tid] = 0; }
             __syncthreads();
-            /* tiers (twin: m loop with q = need[m] - red) */
+            /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
+            const int32_t hv = (lane + 1 <= R) ? Hc[lane + 1] : 0;
+            const int32_t S0 = wave_sufscan(hv);
+            const int32_t S1 = wave_sufscan(hv * (lane + 1));
+            const int32_t need = (lane < R) ? (S1 - lane * S0) - G * (R - 1 - lane) : -1;
             int mstart = R - 1;
-            while (true) {
-                if (threadIdx.x == 0) {
-                    int mf = -1;
-                    int64_t qf = 0, red = 0;
-                    for (int v = mstart + 1; v <= R; ++v) red += SH[v];
-                    for (int m = mstart; m >= 0; --m) {
-                        int64_t qq = need[m] - red;
-                        if (qq > 0) { mf = m; qf = qq; break; }
-                        red += SH[m];
-                    }
-                    misc[0] = mf;
-                    misc[1] = qf;
-                }
-                __syncthreads();
-                const int m = (int)misc[0];
-                const int64_t qv = misc[1];
-                __syncthreads();
-                if (m < 0) break;
-                int32_t lv = 0;
-                for (int i = plo; i < phi; ++i) {
-                    int rr = rpos[i] < R ? rpos[i] : R;
-                    if (!selp[i] && rr > m) lv += wpos[i];
+            while (mstart >= 0) {
+                const int32_t shv = (lane + 1 <= R) ? SHc[lane + 1] : 0;
+                const int32_t red = wave_sufscan(shv);
+                const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
+                if (mask == 0) break;
+                const int m = 63 - __builtin_clzll(mask);
+                const int32_t q = __shfl(need - red, m, 64);
+                int32_t lt = 0;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
+                    if (2 * tid + i < A_ && !st_sel(st[i]) && rr > m) lt += (int32_t)st_w(st[i]);
                 }
                 int32_t tot;
-                int64_t ex = block_exscan_i32(lv, &tot, S);
-                int64_t took_l = 0;
-                for (int i = plo; i < phi; ++i) {
-                    int rr = rpos[i] < R ? rpos[i] : R;
-                    if (!selp[i] && rr > m) {
-                        if (ex < qv && ex + wpos[i] <= cap) {
-                            selp[i] = 1;
-                            atomicAdd(&SH[rr], (int32_t)wpos[i]);
-                            took_l += wpos[i];
+                int32_t ex = blk.exscan(lt, tot);
+                int32_t took = 0;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
+                    if (2 * tid + i < A_ && !st_sel(st[i]) && rr > m) {
+                        const int32_t w = (int32_t)st_w(st[i]);
+                        if (ex < q && ex + w <= cap) {
+                            st[i] |= (1u << 16);
+                            atomicAdd(&SHc[rr], w);
+                            took += w;
                         }
-                        ex += wpos[i];
+                        ex += w;
                     }
                 }
-                cap -= block_sum(took_l, S);
+                cap -= blk.sum32(took);
                 mstart = m - 1;
             }
-            /* fill */
             {
-                int32_t lv = 0;
-                for (int i = plo; i < phi; ++i)
-                    if (!selp[i] && rpos[i] > 0) lv += wpos[i];
+                int32_t lt = 0;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) lt += (int32_t)st_w(st[i]);
                 int32_t tot;
-                int64_t ex = block_exscan_i32(lv, &tot, S);
-                int64_t took_l = 0;
-                for (int i = plo; i < phi; ++i) {
-                    if (!selp[i] && rpos[i] > 0) {
-                        if (ex + wpos[i] <= cap) { selp[i] = 1; took_l += wpos[i]; }
-                        ex += wpos[i];
+                int32_t ex = blk.exscan(lt, tot);
+                int32_t took = 0;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) {
+                        const int32_t w = (int32_t)st_w(st[i]);
+                        if (ex + w <= cap) { st[i] |= (1u << 16); took += w; }
+                        ex += w;
                     }
                 }
-                cap -= block_sum(took_l, S);
+                cap -= blk.sum32(took);
             }
-            /* width tail */
+            /* width tail: first position in order that still fits; the key
+             * carries (position << 4 | w) so the min also names the width */
             while (cap > 0) {
-                uint64_t best = 0;
-                for (int i = plo; i < phi; ++i)
-                    if (!selp[i] && rpos[i] > 0 && (int64_t)wpos[i] <= cap) {
-                        uint64_t key = (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
-                        best = key > best ? key : best;
-                    }
-                best = block_max_u64(best, S);
-                if (best == 0) break;
-                const int pick = (int)(0xFFFFFFFFu - (uint32_t)best);
-                if (pick >= plo && pick < phi) selp[pick] = 1;
-                cap -= wpos[pick];
+                int32_t best = 0x7FFFFFFF;
+#pragma unroll
+                for (int i = 1; i >= 0; --i) {
+                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0 && (int32_t)st_w(st[i]) <= cap)
+                        best = ((2 * tid + i) << 4) | (int32_t)st_w(st[i]);
+                }
+                best = blk.min32(best);
+                if (best == 0x7FFFFFFF) break;
+                const int pos = best >> 4;
+                if ((pos >> 1) == tid) st[pos & 1] |= (1u << 16);
+                cap -= best & 15;
             }
-            for (int i = plo; i < phi; ++i) {
-                if (selp[i]) {
-                    y[ordj[i]] |= (1ull << t);
-                    rpos[i] = (uint8_t)(rpos[i] - 1);
-                    selp[i] = 0;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (2 * tid + i < A_ && st_sel(st[i])) {
+                    mk[i] |= (1ull << t);
+                    st[i] = (st[i] & 0xFF00u) | (st_r(st[i]) - 1u);
                 }
             }
-            __syncthreads();
         }
-        for (int j = jlo(); j < jhi(); ++j) placed_out[j] = 0;
         __syncthreads();
-        for (int i = plo; i < phi; ++i) placed_out[ordj[i]] = (uint8_t)(nin[ordj[i]] - rpos[i]);
-        __syncthreads();
+    }
+
+    /* !ONE: the same loop over position state in the HBM workspace. */
+    __device__ __forceinline__ void rounds_mem(int A_, int PPL) {
+        const int lane = lane_id();
+        /* lane owns positions p = lane·PPL + i, i < cnt; slot(p) = i·64 + lane */
+        const int p0 = lane * PPL;
+        const int cnt_l = (p0 + PPL < A_ ? p0 + PPL : A_) - p0;
+        const int my = cnt_l > 0 ? cnt_l : 0;
+        for (int t = 0; t < T; ++t) {
+            const int R = T - t;
+            int64_t cap = G;
+            H[lane] = 0;
+            SH[lane] = 0;
+            if (lane == 0) { H[64] = 0; SH[64] = 0; }
+            wave_sync();
+            for (int i = 0; i < my; ++i) {
+                const uint32_t s = pst[i * 64 + lane];
+                const int rr = (int)st_r(s) < R ? (int)st_r(s) : R;
+                atomicAdd(&H[rr], (int32_t)st_w(s));
+            }
+            wave_sync();
+            /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m); lane m holds m */
+            const int64_t hv = (lane + 1 <= R) ? (int64_t)H[lane + 1] : 0;
+            const int64_t S0 = wave_sufscan(hv);
+            const int64_t S1 = wave_sufscan(hv * (int64_t)(lane + 1));
+            const int64_t need = (lane < R)
+                                     ? (S1 - (int64_t)lane * S0) - (int64_t)G * (R - 1 - lane)
+                                     : (int64_t)-1;
+            /* tiers, highest m first */
+            int mstart = R - 1;
+            while (mstart >= 0) {
+                const int64_t shv = (lane + 1 <= R) ? (int64_t)SH[lane + 1] : 0;
+                const int64_t red = wave_sufscan(shv);
+                const int64_t qv = need - red;
+                const uint64_t mask = __ballot(lane <= mstart && qv > 0);
+                if (mask == 0) break;
+                const int m = 63 - __builtin_clzll(mask);
+                const int64_t q = __shfl(qv, m, 64);
+                int32_t lt = 0;
+                for (int i = 0; i < my; ++i) {
+                    const uint32_t s = pst[i * 64 + lane];
+                    const int rr = (int)st_r(s) < R ? (int)st_r(s) : R;
+                    if (!st_sel(s) && rr > m) lt += (int32_t)st_w(s);
+                }
+                int64_t ex = (int64_t)(wave_incscan(lt) - lt);
+                int32_t took = 0;
+                for (int i = 0; i < my; ++i) {
+                    const int sl = i * 64 + lane;
+                    const uint32_t s = pst[sl];
+                    const int rr = (int)st_r(s) < R ? (int)st_r(s) : R;
+                    if (!st_sel(s) && rr > m) {
+                        const int64_t w = st_w(s);
+                        if (ex < q && ex + w <= cap) {
+                            pst[sl] = s | (1u << 16);
+                            atomicAdd(&SH[rr], (int32_t)w);
+                            took += (int32_t)w;
+                        }
+                        ex += w;
+                    }
+                }
+                cap -= wave_sum(took);
+                wave_sync();
+                mstart = m - 1;
+            }
+            /* fill in order */
+            {
+                int32_t lt = 0;
+                for (int i = 0; i < my; ++i) {
+                    const uint32_t s = pst[i * 64 + lane];
+                    if (!st_sel(s) && st_r(s) > 0) lt += (int32_t)st_w(s);
+                }
+                int64_t ex = (int64_t)(wave_incscan(lt) - lt);
+                int32_t took = 0;
+                for (int i = 0; i < my; ++i) {
+                    const int sl = i * 64 + lane;
+                    const uint32_t s = pst[sl];
+                    if (!st_sel(s) && st_r(s) > 0) {
+                        const int64_t w = st_w(s);
+                        if (ex + w <= cap) { pst[sl] = s | (1u << 16); took += (int32_t)w; }
+                        ex += w;
+                    }
+                }
+                cap -= wave_sum(took);
+                wave_sync();
+            }
+            /* width tail: first position in order that still fits */
+            while (cap > 0) {
+                int first = 0x7FFFFFFF;
+                for (int i = 0; i < my; ++i) {
+                    const uint32_t s = pst[i * 64 + lane];
+                    if (!st_sel(s) && st_r(s) > 0 && (int64_t)st_w(s) <= cap) { first = p0 + i; break; }
+                }
+                first = wave_min(first);
+                if (first == 0x7FFFFFFF) break;
+                const int owner = first / PPL;
+                const int sl = (first - owner * PPL) * 64 + owner;
+                const uint32_t s = pst[sl];
+                wave_sync();
+                if (lane == owner) pst[sl] = s | (1u << 16);
+                cap -= st_w(s);
+                wave_sync();
+            }
+            /* apply: selected positions run in round t */
+            for (int i = 0; i < my; ++i) {
+                const int sl = i * 64 + lane;
+                const uint32_t s = pst[sl];
+                if (st_sel(s)) {
+                    pmask[sl] |= (1ull << t);
+                    pst[sl] = (s & 0xFF00u) | (st_r(s) - 1u);
+                }
+            }
+            wave_sync();
+        }
     }
 };
 
@@ -546,20 +875,19 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.w_in = B.w + jo;
     c.p_in = B.p + jo;
 
-    /* LDS carve-up (16-byte aligned pieces) */
     size_t off = 0;
     auto carve = [&](size_t bytes) {
         unsigned char* p = smem + off;
         off += (bytes + 15) & ~(size_t)15;
         return p;
     };
-    c.S = (sw_scratch*)carve(sizeof(sw_scratch));
+    c.blk.X = (sw_xchg*)carve(sizeof(sw_xchg));
+    c.blk.par = 0;
     double* bt = (double*)carve(sizeof(double) * 2 * SW_BMAX);
     c.beta = bt;
     c.ell = bt + SW_BMAX;
-    c.H = (int32_t*)carve(sizeof(int32_t) * (SW_TMAX + 2));
-    c.SH = (int32_t*)carve(sizeof(int32_t) * (SW_TMAX + 2));
-    c.need = (int64_t*)carve(sizeof(int64_t) * SW_TMAX);
+    c.H = (int32_t*)carve(sizeof(int32_t) * 136);
+    c.SH = (int32_t*)carve(sizeof(int32_t) * 136);
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
     if (threadIdx.x < SW_BMAX) {
         bt[threadIdx.x] = I->beta[threadIdx.x];
@@ -574,23 +902,23 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.placed = carve(NJ);
         c.placed2 = carve(NJ);
         c.nfin = carve(NJ);
-        c.rpos = carve(NJ);
-        c.wpos = carve(NJ);
-        c.selp = carve(NJ);
-        c.ordj = (int32_t*)carve(sizeof(int32_t) * NJ);
+        c.pst = (uint32_t*)carve(sizeof(uint32_t) * NJ);
+        c.pord = (int32_t*)carve(sizeof(int32_t) * NJ);
+        c.pmask = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.ybest = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
-        c.shi = (uint64_t*)carve(sizeof(uint64_t) * NJ);
-        c.slo = (uint64_t*)carve(sizeof(uint64_t) * NJ);
+        c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 8 * SW_BLOCK);
         c.gkeys = nullptr;
         c.gjc = nullptr;
-        const int j = (int)threadIdx.x;
-        if (j < N) {
-            c.jc0 = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
-                                 B.E[jo + j], B.R[jo + j], B.p[jo + j]);
-        } else {
-            c.jc0 = sw_make_jobc(1, 1, 1.0, 1, 1.0, 0, 1, 0.0, 0.0);
+#pragma unroll
+        for (int s = 0; s < SW_JPT; ++s) {
+            const int j = c.jlo() + s;
+            if (s < c.q && j < N)
+                c.jcs[s] = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
+                                        B.E[jo + j], B.R[jo + j], B.p[jo + j]);
+            else
+                c.jcs[s] = sw_make_jobc(1, 1, 1.0, 1, 1.0, 0, 1, 0.0, 0.0);
         }
     } else {
         uint8_t* u8 = B.ws.u8 + SW_WS_U8 * jo;
@@ -599,18 +927,16 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.tkcur = u8 + 2 * (size_t)N;
         c.nbest = u8 + 3 * (size_t)N;
         c.placed = u8 + 4 * (size_t)N;
-        c.nfin = u8 + 5 * (size_t)N;
-        c.rpos = u8 + 6 * (size_t)N;
-        c.wpos = u8 + 7 * (size_t)N;
-        c.selp = u8 + 8 * (size_t)N;
-        c.placed2 = u8 + 9 * (size_t)N;
-        uint64_t* m64 = B.ws.u64 + 4 * jo;
+        c.placed2 = u8 + 5 * (size_t)N;
+        c.nfin = u8 + 6 * (size_t)N;
+        uint64_t* m64 = B.ws.u64 + SW_WS_U64 * jo;
         c.ycur = m64;
         c.ybest = m64 + N;
         c.y2 = m64 + 2 * (size_t)N;
-        c.ordj = (int32_t*)(m64 + 3 * (size_t)N); /* N int32 fit in N u64 */
-        c.shi = B.ws.sort + 4 * jo;
-        c.slo = c.shi + 2 * (size_t)N;
+        c.pmask = m64 + 3 * (size_t)N;
+        c.pst = (uint32_t*)(m64 + 4 * (size_t)N);
+        c.pord = (int32_t*)(m64 + 5 * (size_t)N);
+        c.sbuf = B.ws.sort + 4 * jo;
         c.gkeys = B.ws.keys + (size_t)KT * jo;
         c.gjc = B.ws.jc + jo;
         for (int j = c.jlo(); j < c.jhi(); ++j)
@@ -619,59 +945,83 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     }
     __syncthreads();
 
+#ifdef SW_STAMPS
+    uint64_t stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
     c.setup();
+    SW_STAMP(0);
 
-    /* ---- P1: level search + packing with budget re-solve (twin: twin_plan_solve) ---- */
+    /* ---- P1: level search + packing with budget re-solve, then P2
+     *      (twin_plan_solve).  One pack call site: requests are
+     *      (mode 1: P1 order A, mode 3: P1 order B, mode 2: P2). ---- */
     int32_t status = 0;
-    double bound = 0.0, Jbest = 0.0;
-    for (int it = 0; it < SW_REPACK_ITERS; ++it) {
-        const double b0 = c.level_search();
-        if (it == 0) bound = b0;
-        /* order A; order B only if A left rounds unplaced (twin: ord loop) */
-        int64_t deficit = 0;
-        double Jp = 0.0;
-        for (int ord = 0; ord < 2; ++ord) {
-            uint8_t* pl = ord ? c.placed2 : c.placed;
-            if (ord == 0) c.template pack<1>(c.nbest, c.ycur, pl);
-            else c.template pack<3>(c.nbest, c.y2, pl);
-            int64_t def_l = 0;
-            double fs = 0.0, gm = 0.0;
-            for (int j = c.jlo(); j < c.jhi(); ++j) {
-                def_l += (int64_t)c.jc(j).w * (c.nbest[j] - pl[j]);
-                fs = fs + c.fval(j, pl[j]);
-                gm = sw_max(gm, c.gval(j, pl[j]));
-            }
-            const int64_t dfc = block_sum(def_l, c.S);
-            const double Jo = block_detsum(fs, c.S) - c.k * block_max_d(gm, c.S);
-            c.passes++;
-            if (ord == 0 || Jo > Jp) {
-                Jp = Jo;
-                deficit = dfc;
-                if (ord == 1) {
-                    for (int j = c.jlo(); j < c.jhi(); ++j) {
-                        c.placed[j] = c.placed2[j];
-                        c.ycur[j] = c.y2[j];
-                    }
-                }
-            }
-            if (ord == 0 && dfc == 0) break;
+    double bound = 0.0, Jbest = 0.0, Jp = 0.0;
+    int64_t deficit = 0;
+    int it = 0, mode = 0; /* mode 0 = run the level search next */
+    bool ok2 = true;
+    while (true) {
+        if (mode == 0) {
+            const double b0 = c.level_search();
+            if (it == 0) bound = b0;
+            SW_STAMP(1);
+            mode = 1;
         }
+        uint8_t* pl = (mode == 3) ? c.placed2 : c.placed;
+        const uint8_t* nin = (mode == 2) ? c.nfin : c.nbest;
+        uint64_t* yd = (mode == 1) ? c.ycur : c.y2;
+        c.pack(mode, nin, yd, pl);
+        if (mode == 2) {
+            SW_STAMP(4);
+            int64_t bad_l = 0;
+            c.for_jobs([&](int j, int s) { (void)s; bad_l += (c.placed[j] != c.nfin[j]); });
+            ok2 = c.blk.sum(bad_l) == 0;
+            break;
+        }
+        int64_t def_l = 0;
+        double fs = 0.0, gm = 0.0;
+        c.for_jobs([&](int j, int s) {
+            def_l += (int64_t)c.jc(j, s).w * (c.nbest[j] - pl[j]);
+            fs = fs + c.fval(j, s, pl[j]);
+            gm = sw_max(gm, c.gval(j, s, pl[j]));
+        });
+        const int64_t dfc = c.blk.sum(def_l);
+        double U, Mx;
+        c.blk.detsum_max(fs, gm, U, Mx);
+        const double Jo = U - c.k * Mx;
+        c.passes++;
+        if (mode == 1 || Jo > Jp) {
+            Jp = Jo;
+            deficit = dfc;
+            if (mode == 3) {
+                c.for_jobs([&](int j, int s) {
+                    (void)s;
+                    c.placed[j] = c.placed2[j];
+                    c.ycur[j] = c.y2[j];
+                });
+            }
+        }
+        if (mode == 1 && dfc != 0) { mode = 3; continue; }
+        /* this repack iteration is complete */
+        SW_STAMP(2);
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
-            for (int j = c.jlo(); j < c.jhi(); ++j) {
+            c.for_jobs([&](int j, int s) {
+                (void)s;
                 c.nfin[j] = c.placed[j];
                 c.ybest[j] = c.ycur[j];
-            }
+            });
         }
-        if (deficit == 0) break;
-        status |= SW_STATUS_P1_REPACKED;
-        c.C -= deficit;
+        ++it;
+        if (deficit == 0 || it >= SW_REPACK_ITERS) {
+            SW_STAMP(3);
+            mode = 2;
+        } else {
+            status |= SW_STATUS_P1_REPACKED;
+            c.C -= deficit;
+            mode = 0;
+        }
+        __syncthreads();
     }
-    /* ---- P2 (twin: priority placement of the same counts) ---- */
-    c.template pack<2>(c.nfin, c.y2, c.placed);
-    int64_t bad_l = 0;
-    for (int j = c.jlo(); j < c.jhi(); ++j) bad_l += (c.placed[j] != c.nfin[j]);
-    const bool ok2 = block_sum(bad_l, c.S) == 0;
     if (!ok2) status |= SW_STATUS_P2_FALLBACK;
 
     /* ---- emit ---- */
@@ -679,12 +1029,12 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     double fs = 0.0, gm = 0.0, p2 = 0.0;
     const int T = c.T;
     uint8_t* plan = B.plan + I->plan_off;
-    for (int j = c.jlo(); j < c.jhi(); ++j) {
+    c.for_jobs([&](int j, int s) {
         const uint64_t m = ok2 ? c.y2[j] : c.ybest[j];
         const int cnt = __popcll(m);
         any_l += (cnt > 0);
-        fs = fs + c.fval(j, cnt);
-        gm = sw_max(gm, c.gval(j, cnt));
+        fs = fs + c.fval(j, s, cnt);
+        gm = sw_max(gm, c.gval(j, s, cnt));
         double term = 0.0;
         if (cnt > 0) {
             int64_t Ssum = 0;
@@ -694,12 +1044,13 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         p2 = p2 + term;
         for (int t = 0; t < T; ++t) plan[(size_t)j * T + t] = (uint8_t)((m >> t) & 1ull);
         B.planned[jo + j] = cnt;
-    }
-    const bool any = block_sum(any_l, c.S) > 0;
+    });
+    const bool any = c.blk.sum(any_l) > 0;
     if (!any) status |= SW_STATUS_NO_PLANNED;
-    const double U = block_detsum(fs, c.S);
-    const double Mact = block_max_d(gm, c.S);
-    const double P2 = block_detsum(p2, c.S);
+    double U, Mact;
+    c.blk.detsum_max(fs, gm, U, Mact);
+    const double P2 = c.blk.detsum(p2);
+    SW_STAMP(5);
     if (threadIdx.x == 0) {
         sw_out_dev o;
         o.objective = U - c.k * Mact;
@@ -724,12 +1075,11 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
 /* LDS bytes the kernel needs (must match the carve-up above). */
 extern "C" size_t sw_plan_kernel_lds_bytes(int one) {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t s = r16(sizeof(sw_scratch)) + r16(sizeof(double) * 2 * SW_BMAX) +
-               2 * r16(sizeof(int32_t) * (SW_TMAX + 2)) + r16(sizeof(int64_t) * SW_TMAX) +
-               r16(sizeof(int64_t) * 8);
+    size_t s = r16(sizeof(sw_xchg)) + r16(sizeof(double) * 2 * SW_BMAX) +
+               2 * r16(sizeof(int32_t) * 136) + r16(sizeof(int64_t) * 8);
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
-        s += 10 * r16(NJ) + r16(4 * NJ) + 5 * r16(8 * NJ);
+        s += 7 * r16(NJ) + 2 * r16(4 * NJ) + 4 * r16(8 * NJ) + r16(8 * 8 * SW_BLOCK);
     }
     return s;
 }

@@ -1,0 +1,47 @@
+"""Per-phase cycle breakdown of the plan kernel (diagnostic build).
+
+    make -C shockwave-replication_amd/csrc stamps && python tools/stamps.py
+
+Phases: 0 setup (constants + key rows), 1 P1 level search, 2 P1 packing
+(both orders), 3 P1 bookkeeping, 4 P2 placement, 5 emit.  s_memtime ticks
+are shader-clock cycles; shares are what matter (stamps add barriers).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "shockwave-replication_amd"))
+import sw_native as sn  # noqa: E402
+import sw_synth as ss  # noqa: E402
+
+
+def main():
+    lib = sn.load(os.path.join(ROOT, "shockwave-replication_amd", "lib", "libshockwave_amd_stamps.so"))
+    lib.sw_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    cases = {
+        "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 64)],
+        "g64_900x20_k1e-3": [ss.synth_problem(i, 900, 64, 20, 120.0, 1e-3, 15.0) for i in range(16)],
+        "g128_120x20_k10": [ss.synth_problem(i, 120, 128, 20, 120.0, 10.0, 5.0) for i in range(16)],
+    }
+    names = ["setup", "p1_level_search", "p1_pack", "p1_misc", "p2_pack", "emit"]
+    for name, batch in cases.items():
+        s = sn.Solver(device=0, lib=lib)
+        s.upload(batch)
+        s.run()
+        res = s.download()
+        st = np.zeros(len(batch) * 8, dtype=np.uint64)
+        lib.sw_debug_stamps(s.h, st.ctypes.data_as(C.POINTER(C.c_uint64)))
+        st = st.reshape(len(batch), 8)[:, :6].astype(np.float64)
+        tot = st.sum(axis=1).mean()
+        print(f"{name}: mean cycles/instance {tot:.0f}; passes {np.mean([r['iters'] for r in res]):.1f}; "
+              f"status {sorted(set(r['status'] for r in res))}")
+        for i, n in enumerate(names):
+            print(f"   {n:16s} {st[:, i].mean():12.0f}  {100 * st[:, i].mean() / tot:5.1f}%")
+        s.close()
+
+
+if __name__ == "__main__":
+    main()
