@@ -245,7 +245,7 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         h->d_planned.reserve(Jz) || h->d_d.reserve(Jz) || h->d_R.reserve(Jz) ||
         h->d_p.reserve(Jz) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
         return fail(h, SW_ERR_HIP, "device allocation failed");
-    if (maxN > SW_LDS_JOBS) {
+    if (maxN > SW_LDS_JOBS || maxT > 32) {
         const int KT = maxT <= 32 ? 32 : 64;
         if (h->d_ws_u8.reserve(Jz * SW_WS_U8) || h->d_ws_u64.reserve(Jz * SW_WS_U64) ||
             h->d_ws_sort.reserve(Jz * 4) || h->d_ws_keys.reserve(Jz * KT) ||
@@ -349,7 +349,7 @@ int sw_batch_run(sw_handle* h) {
 #ifdef SW_STAMPS
     B.stamps = h->d_stamps.p;
 #endif
-    const int one = h->maxN <= SW_LDS_JOBS;
+    const int one = h->maxN <= SW_LDS_JOBS && h->maxT <= 32;
     if (!one) {
         B.ws.u8 = h->d_ws_u8.p;
         B.ws.u64 = h->d_ws_u64.p;

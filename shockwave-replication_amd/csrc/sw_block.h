@@ -35,6 +35,50 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+/* ---- DPP (data-parallel primitives) integer scans ----------------------
+ * Hillis-Steele inside each 16-lane row with row_shr:1/2/4/8, then
+ * row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) — the GFX9-family
+ * cross-row steps that gfx950 keeps.  Each step is one v_add with a DPP
+ * source operand (a few cycles), instead of a ds_bpermute round trip
+ * through the LDS crossbar.  Integer ops only (associative, so the order
+ * does not matter). */
+__device__ __forceinline__ int32_t dpp_incscan_i32(int32_t x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false); /* row_shr:1 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false); /* row_shr:2 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false); /* row_shr:4 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false); /* row_shr:8 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false); /* row_bcast:15 */
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false); /* row_bcast:31 */
+    return x;
+}
+__device__ __forceinline__ int32_t dpp_incmax_i32(int32_t x) {
+    const int32_t lo = INT32_MIN;
+    int32_t y;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x111, 0xF, 0xF, false); x = y > x ? y : x;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x112, 0xF, 0xF, false); x = y > x ? y : x;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x114, 0xF, 0xF, false); x = y > x ? y : x;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x118, 0xF, 0xF, false); x = y > x ? y : x;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x142, 0xA, 0xF, false); x = y > x ? y : x;
+    y = __builtin_amdgcn_update_dpp(lo, x, 0x143, 0xC, 0xF, false); x = y > x ? y : x;
+    return x;
+}
+/* wave-wide results (uniform, via v_readlane of lane 63) */
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
+    return __builtin_amdgcn_readlane(dpp_incscan_i32(v), 63);
+}
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
+    return __builtin_amdgcn_readlane(dpp_incmax_i32(v), 63);
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+    return -wave_max_i32(-v);
+}
+/* inclusive prefix / suffix over lanes */
+__device__ __forceinline__ int32_t wave_incscan_i32(int32_t v) { return dpp_incscan_i32(v); }
+__device__ __forceinline__ int32_t wave_sufscan_i32(int32_t v) {
+    const int32_t inc = dpp_incscan_i32(v);
+    return __builtin_amdgcn_readlane(inc, 63) - inc + v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -104,7 +148,7 @@ struct sw_blk {
     __device__ __forceinline__ void flip() { par ^= 1; }
 
     __device__ __forceinline__ int32_t sum32(int32_t v) {
-        v = wave_sum(v);
+        v = wave_sum_i32(v);
         if (lane_id() == 0) X->s[par][wave_id()] = v;
         __syncthreads();
         int32_t t = 0;
@@ -115,7 +159,7 @@ struct sw_blk {
     }
 
     __device__ __forceinline__ int32_t min32(int32_t v) {
-        v = wave_min(v);
+        v = wave_min_i32(v);
         if (lane_id() == 0) X->s[par][wave_id()] = v;
         __syncthreads();
         int32_t t = X->s[par][0];
@@ -125,20 +169,22 @@ struct sw_blk {
         return t;
     }
 
+    /* 64-bit sums of values that fit in 32 bits per wave (all callers sum
+     * weighted counts ≤ 2^31 per wave) */
     __device__ __forceinline__ int64_t sum(int64_t v) {
-        v = wave_sum(v);
-        if (lane_id() == 0) X->i[par][wave_id()][0] = v;
+        const int64_t w = wave_sum_i32((int32_t)v);
+        if (lane_id() == 0) X->i[par][wave_id()][0] = w;
         __syncthreads();
         int64_t t = 0;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) t += X->i[par][w][0];
+        for (int k = 0; k < SW_WAVES; ++k) t += X->i[par][k][0];
         flip();
         return t;
     }
 
     __device__ __forceinline__ void sum2(int64_t a, int64_t b, int64_t& ra, int64_t& rb) {
-        a = wave_sum(a);
-        b = wave_sum(b);
+        a = wave_sum_i32((int32_t)a);
+        b = wave_sum_i32((int32_t)b);
         if (lane_id() == 0) { X->i[par][wave_id()][0] = a; X->i[par][wave_id()][1] = b; }
         __syncthreads();
         int64_t ta = 0, tb = 0;
@@ -201,7 +247,7 @@ struct sw_blk {
 
     /* Exclusive prefix sum over thread order; also returns the total. */
     __device__ __forceinline__ int32_t exscan(int32_t v, int32_t& total) {
-        int32_t x = wave_incscan(v);
+        int32_t x = wave_incscan_i32(v);
         if (lane_id() == 63) X->s[par][wave_id()] = x;
         __syncthreads();
         int32_t base = 0, tot = 0;

@@ -60,7 +60,7 @@ __device__ __forceinline__ uint32_t st_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t st_w(uint32_t s) { return (s >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t st_sel(uint32_t s) { return (s >> 16) & 1u; }
 
-/* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = 2 · SW_BLOCK) */
+/* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = SW_JPT · SW_BLOCK) */
 #define SW_JPT 2
 
 template <int KT, bool ONE>
@@ -200,8 +200,9 @@ struct Ctx {
         for_jobs([&](int j, int s) { amax = sw_max(amax, jc(j, s).a); });
         A = blk.dmax(amax);
         if constexpr (ONE) {
-            /* rolled evaluation into an LDS staging window (8 keys × 2 jobs
+            /* rolled evaluation into an LDS staging window (4 keys × 4 jobs
              * per thread per chunk), then compile-time-indexed copies */
+            constexpr int CH = 4;
             float* stage = reinterpret_cast<float*>(sbuf);
             double prev[SW_JPT], vm[SW_JPT];
 #pragma unroll
@@ -211,12 +212,12 @@ struct Ctx {
                 if (s < q && jlo() + s < N) prev[s] = sw_f(&jcs[s], 0, nb, beta, ell);
             }
 #pragma unroll
-            for (int ch = 0; ch < KT / 8; ++ch) {
+            for (int ch = 0; ch < KT / CH; ++ch) {
 #pragma unroll
                 for (int s = 0; s < SW_JPT; ++s) {
                     const bool act = s < q && jlo() + s < N;
-                    for (int i = 0; i < 8; ++i) {
-                        const int n = ch * 8 + i;
+                    for (int i = 0; i < CH; ++i) {
+                        const int n = ch * CH + i;
                         float kv = 0.0f;
                         if (act && n < T && jcs[s].w <= G) {
                             const double cur = sw_f(&jcs[s], n + 1, nb, beta, ell);
@@ -225,14 +226,14 @@ struct Ctx {
                             kv = sw_key(vm[s], jcs[s].w, A);
                             prev[s] = cur;
                         }
-                        stage[(s * 8 + i) * SW_BLOCK + threadIdx.x] = kv;
+                        stage[(s * CH + i) * SW_BLOCK + threadIdx.x] = kv;
                     }
                 }
 #pragma unroll
                 for (int s = 0; s < SW_JPT; ++s)
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        kr[s][ch * 8 + i] = stage[(s * 8 + i) * SW_BLOCK + threadIdx.x];
+                    for (int i = 0; i < CH; ++i)
+                        kr[s][ch * CH + i] = stage[(s * CH + i) * SW_BLOCK + threadIdx.x];
             }
         } else {
             for (int j = jlo(); j < jhi(); ++j) {
@@ -446,49 +447,58 @@ struct Ctx {
     /* position p (of A, PPL per lane of wave 0) → transposed slot */
     __device__ __forceinline__ int tslot(int p, int PPL) const { return (p % PPL) * 64 + p / PPL; }
 
-    /* Sort (hi, lo) descending.  ONE: register bitonic over 1024 elements,
-     * two per thread (element e = 2·tid + s).  Stride 1 compares inside the
-     * thread, strides 2 … 64 pair threads of one wave (shuffles), larger
-     * strides go through a double-buffered LDS exchange (one barrier per
-     * stage).  After the sort thread t holds positions 2t and 2t + 1. */
-    __device__ __forceinline__ void sort_regs(uint64_t (&hi)[2], uint64_t (&lo)[2]) {
+    /* Sort (hi, lo) descending.  ONE: register bitonic over E·SW_BLOCK =
+     * 1024 elements, E per thread (element e = E·tid + s).  Strides < E
+     * compare inside the thread, strides E … 32·E pair threads of one wave
+     * (shuffles), larger strides go through a double-buffered LDS exchange
+     * (one barrier per stage).  After the sort thread t holds positions
+     * E·t … E·t + E − 1. */
+    __device__ __forceinline__ void sort_regs(uint64_t (&hi)[SW_JPT], uint64_t (&lo)[SW_JPT]) {
+        constexpr int E = SW_JPT;
+        constexpr int NE = E * SW_BLOCK;
         const int tid = threadIdx.x;
         int buf = 0;
-        for (int kk = 2; kk <= 2 * SW_BLOCK; kk <<= 1) {
+        for (int kk = 2; kk <= NE; kk <<= 1) {
             for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-                if (jj == 1) {
-                    const bool up = ((2 * tid) & kk) == 0;
-                    const bool gt = (hi[0] > hi[1]) || (hi[0] == hi[1] && lo[0] > lo[1]);
-                    if (up ? !gt : gt) {
-                        const uint64_t th = hi[0], tl = lo[0];
-                        hi[0] = hi[1]; lo[0] = lo[1]; hi[1] = th; lo[1] = tl;
+                if (jj < E) {
+#pragma unroll
+                    for (int s = 0; s < E; ++s) {
+                        if ((s & jj) == 0) {
+                            const int t2 = s | jj;
+                            const bool up = ((E * tid + s) & kk) == 0;
+                            const bool gt = (hi[s] > hi[t2]) || (hi[s] == hi[t2] && lo[s] > lo[t2]);
+                            if (up ? !gt : gt) {
+                                const uint64_t th = hi[s], tl = lo[s];
+                                hi[s] = hi[t2]; lo[s] = lo[t2]; hi[t2] = th; lo[t2] = tl;
+                            }
+                        }
                     }
                     continue;
                 }
-                uint64_t ph[2], pl[2];
-                const int tj = jj >> 1;
+                uint64_t ph[E], pl[E];
+                const int tj = jj / E;
                 if (tj >= 64) {
-                    uint64_t* xh = sbuf + (size_t)buf * 4 * SW_BLOCK;
-                    uint64_t* xl = xh + 2 * SW_BLOCK;
+                    uint64_t* xh = sbuf + (size_t)buf * 2 * NE;
+                    uint64_t* xl = xh + NE;
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) { xh[2 * tid + s] = hi[s]; xl[2 * tid + s] = lo[s]; }
+                    for (int s = 0; s < E; ++s) { xh[E * tid + s] = hi[s]; xl[E * tid + s] = lo[s]; }
                     __syncthreads();
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        ph[s] = xh[(2 * tid + s) ^ jj];
-                        pl[s] = xl[(2 * tid + s) ^ jj];
+                    for (int s = 0; s < E; ++s) {
+                        ph[s] = xh[(E * tid + s) ^ jj];
+                        pl[s] = xl[(E * tid + s) ^ jj];
                     }
                     buf ^= 1;
                 } else {
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) {
+                    for (int s = 0; s < E; ++s) {
                         ph[s] = __shfl_xor(hi[s], tj, 64);
                         pl[s] = __shfl_xor(lo[s], tj, 64);
                     }
                 }
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int e = 2 * tid + s;
+                for (int s = 0; s < E; ++s) {
+                    const int e = E * tid + s;
                     const bool up = (e & kk) == 0;
                     const bool lower = (e & jj) == 0;
                     const bool mine_gt = (hi[s] > ph[s]) || (hi[s] == ph[s] && lo[s] > pl[s]);
@@ -559,7 +569,10 @@ struct Ctx {
         }
         int64_t act_l = 0;
         if constexpr (ONE) {
-            uint64_t khi[2] = {0, 0}, klo[2] = {0, 0};
+            constexpr int E = SW_JPT;
+            uint64_t khi[E], klo[E];
+#pragma unroll
+            for (int s = 0; s < E; ++s) { khi[s] = 0; klo[s] = 0; }
             for_jobs([&](int j, int s) {
                 key_of(MODE, nin, Mb, j, s, khi[s], klo[s]);
                 act_l += nin[j] > 0;
@@ -567,12 +580,13 @@ struct Ctx {
             });
             const int A_ = (int)blk.sum(act_l);
             sort_regs(khi, klo);
-            uint32_t st[2];
-            uint64_t mk[2] = {0, 0};
-            int jp[2];
+            uint32_t st[E];
+            uint64_t mk[E];
+            int jp[E];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int p = 2 * (int)threadIdx.x + s;
+            for (int s = 0; s < E; ++s) {
+                const int p = E * (int)threadIdx.x + s;
+                mk[s] = 0;
                 jp[s] = (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
                 st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | ((uint32_t)w_in[jp[s]] << 8)) : 0u;
             }
@@ -580,8 +594,8 @@ struct Ctx {
             for_jobs([&](int j, int s) { (void)s; placed_out[j] = 0; });
             __syncthreads();
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int p = 2 * (int)threadIdx.x + s;
+            for (int s = 0; s < E; ++s) {
+                const int p = E * (int)threadIdx.x + s;
                 if (p < A_) {
                     y[jp[s]] = mk[s];
                     placed_out[jp[s]] = (uint8_t)(nin[jp[s]] - st_r(st[s]));
@@ -635,10 +649,12 @@ struct Ctx {
         rounds_mem(A_, PPL);
     }
 
-    /* ONE: all 8 waves; thread t keeps its positions 2t, 2t+1 (as left by
-     * the sort) in VGPRs.  Block scans/sums take one barrier each; the
+    /* ONE: all waves; thread t keeps its positions E·t … E·t+E−1 (as left
+     * by the sort) in VGPRs.  Block scans/sums take one barrier each; the
      * histograms H/SH are double-buffered by round parity. */
-    __device__ __forceinline__ void rounds_block(int A_, uint32_t (&st)[2], uint64_t (&mk)[2]) {
+    __device__ __forceinline__ void rounds_block(int A_, uint32_t (&st)[SW_JPT],
+                                                 uint64_t (&mk)[SW_JPT]) {
+        constexpr int E = SW_JPT;
         const int tid = threadIdx.x;
         const int lane = lane_id();
         int32_t* Hb[2] = {H, H + 68};
@@ -651,8 +667,8 @@ struct Ctx {
             int32_t* SHc = SHb[t & 1];
             int32_t cap = G;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (2 * tid + i < A_) {
+            for (int i = 0; i < E; ++i) {
+                if (E * tid + i < A_) {
                     const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
                     atomicAdd(&Hc[rr], (int32_t)st_w(st[i]));
                 }
@@ -662,30 +678,30 @@ struct Ctx {
             __syncthreads();
             /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
             const int32_t hv = (lane + 1 <= R) ? Hc[lane + 1] : 0;
-            const int32_t S0 = wave_sufscan(hv);
-            const int32_t S1 = wave_sufscan(hv * (lane + 1));
+            const int32_t S0 = wave_sufscan_i32(hv);
+            const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
             const int32_t need = (lane < R) ? (S1 - lane * S0) - G * (R - 1 - lane) : -1;
             int mstart = R - 1;
             while (mstart >= 0) {
                 const int32_t shv = (lane + 1 <= R) ? SHc[lane + 1] : 0;
-                const int32_t red = wave_sufscan(shv);
+                const int32_t red = wave_sufscan_i32(shv);
                 const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
                 if (mask == 0) break;
                 const int m = 63 - __builtin_clzll(mask);
                 const int32_t q = __shfl(need - red, m, 64);
                 int32_t lt = 0;
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
+                for (int i = 0; i < E; ++i) {
                     const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
-                    if (2 * tid + i < A_ && !st_sel(st[i]) && rr > m) lt += (int32_t)st_w(st[i]);
+                    if (E * tid + i < A_ && !st_sel(st[i]) && rr > m) lt += (int32_t)st_w(st[i]);
                 }
                 int32_t tot;
                 int32_t ex = blk.exscan(lt, tot);
                 int32_t took = 0;
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
+                for (int i = 0; i < E; ++i) {
                     const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
-                    if (2 * tid + i < A_ && !st_sel(st[i]) && rr > m) {
+                    if (E * tid + i < A_ && !st_sel(st[i]) && rr > m) {
                         const int32_t w = (int32_t)st_w(st[i]);
                         if (ex < q && ex + w <= cap) {
                             st[i] |= (1u << 16);
@@ -701,14 +717,14 @@ struct Ctx {
             {
                 int32_t lt = 0;
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) lt += (int32_t)st_w(st[i]);
+                for (int i = 0; i < E; ++i)
+                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) lt += (int32_t)st_w(st[i]);
                 int32_t tot;
                 int32_t ex = blk.exscan(lt, tot);
                 int32_t took = 0;
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) {
+                for (int i = 0; i < E; ++i) {
+                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) {
                         const int32_t w = (int32_t)st_w(st[i]);
                         if (ex + w <= cap) { st[i] |= (1u << 16); took += w; }
                         ex += w;
@@ -721,19 +737,23 @@ struct Ctx {
             while (cap > 0) {
                 int32_t best = 0x7FFFFFFF;
 #pragma unroll
-                for (int i = 1; i >= 0; --i) {
-                    if (2 * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0 && (int32_t)st_w(st[i]) <= cap)
-                        best = ((2 * tid + i) << 4) | (int32_t)st_w(st[i]);
+                for (int i = E - 1; i >= 0; --i) {
+                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0 && (int32_t)st_w(st[i]) <= cap)
+                        best = ((E * tid + i) << 4) | (int32_t)st_w(st[i]);
                 }
                 best = blk.min32(best);
                 if (best == 0x7FFFFFFF) break;
                 const int pos = best >> 4;
-                if ((pos >> 1) == tid) st[pos & 1] |= (1u << 16);
+                if (pos / E == tid) {
+#pragma unroll
+                    for (int i = 0; i < E; ++i)
+                        if (i == pos % E) st[i] |= (1u << 16);
+                }
                 cap -= best & 15;
             }
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (2 * tid + i < A_ && st_sel(st[i])) {
+            for (int i = 0; i < E; ++i) {
+                if (E * tid + i < A_ && st_sel(st[i])) {
                     mk[i] |= (1ull << t);
                     st[i] = (st[i] & 0xFF00u) | (st_r(st[i]) - 1u);
                 }
@@ -902,13 +922,13 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.placed = carve(NJ);
         c.placed2 = carve(NJ);
         c.nfin = carve(NJ);
-        c.pst = (uint32_t*)carve(sizeof(uint32_t) * NJ);
-        c.pord = (int32_t*)carve(sizeof(int32_t) * NJ);
-        c.pmask = (uint64_t*)carve(sizeof(uint64_t) * NJ);
+        c.pst = nullptr;
+        c.pord = nullptr;
+        c.pmask = nullptr;
         c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.ybest = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
-        c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 8 * SW_BLOCK);
+        c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 4 * SW_JPT * SW_BLOCK);
         c.gkeys = nullptr;
         c.gjc = nullptr;
 #pragma unroll
@@ -1079,7 +1099,7 @@ extern "C" size_t sw_plan_kernel_lds_bytes(int one) {
                2 * r16(sizeof(int32_t) * 136) + r16(sizeof(int64_t) * 8);
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
-        s += 7 * r16(NJ) + 2 * r16(4 * NJ) + 4 * r16(8 * NJ) + r16(8 * 8 * SW_BLOCK);
+        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
     }
     return s;
 }
@@ -1091,8 +1111,9 @@ extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, siz
         if (one) hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, lds, stream, *B);
         else hipLaunchKernelGGL((sw_plan_kernel<32, false>), grid, block, lds, stream, *B);
     } else {
-        if (one) hipLaunchKernelGGL((sw_plan_kernel<64, true>), grid, block, lds, stream, *B);
-        else hipLaunchKernelGGL((sw_plan_kernel<64, false>), grid, block, lds, stream, *B);
+        /* T > 32: key rows live in the HBM workspace (a 4×64 register row
+         * would not fit the on-chip budget) */
+        hipLaunchKernelGGL((sw_plan_kernel<64, false>), grid, block, lds, stream, *B);
     }
     return hipGetLastError();
 }
