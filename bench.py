@@ -45,6 +45,24 @@ def pass_bytes(N: int, T: int) -> int:
     return 4 * N * T + 32 * N
 
 
+def pmc_traffic(batch: int, jobs: int, rounds: int):
+    """HBM bytes per batched launch from the committed rocprofv3 PMC passes
+    (profiles/*_summary.json, FETCH_SIZE ×2 per the gfx950 note + WRITE_SIZE),
+    when they were collected on this exact workload; else None."""
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        w = d.get("workload", {})
+        if w.get("instances") == batch and w.get("jobs") == jobs and w.get("rounds") == rounds:
+            best = (d.get("hbm_bytes_per_launch_fetch_x2"), os.path.relpath(path, ROOT))
+    return best
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,6 +173,7 @@ def main():
     alg_bytes = float(np.sum(iters) * pass_bytes(args.jobs, args.rounds))
     achieved = alg_bytes / avg_kernel_s if avg_kernel_s > 0 else 0.0
 
+    traffic = pmc_traffic(args.batch, args.jobs, args.rounds)
     if rank == 0:
         cpu = None
         if args.cpu_baseline:
@@ -188,7 +207,10 @@ def main():
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
-                "traffic": None,
+                "traffic": traffic[0] if traffic else None,
+                "traffic_source": traffic[1] if traffic else None,
+                "note": ("achieved counts the per-pass working set, which stays on chip "
+                         "(VGPR/LDS); traffic is the HBM side (PMC). DESIGN.md §6"),
                 "kernel": "sw_plan_kernel",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "passes_per_instance": float(np.mean(iters)),
