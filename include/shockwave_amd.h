@@ -40,6 +40,7 @@ extern "C" {
 /* Limits of this build. */
 #define SW_MAX_ROUNDS 64 /* future_rounds T (reference configs use 20 and 30) */
 #define SW_MAX_BASES 8   /* len(log_approximation_bases) (reference: 6)        */
+#define SW_MAX_WIDTH 255 /* nworkers of a job that fits the cluster (traces: 1-8) */
 
 /* Return / status codes. */
 #define SW_OK 0
@@ -170,20 +171,51 @@ int sw_set_timing(sw_handle* h, int32_t enable);
 int sw_kernel_times(sw_handle* h, double* ms_rows, double* ms_plan, int32_t* runs);
 
 /*
- * Sharded single instance (jobs split across ranks, one process per GPU).
- * The aggregate weight/count reductions of every price/level step are summed
- * across ranks with ncclAllReduce over xGMI.  unique_id points to
- * SW_NCCL_UNIQUE_ID_BYTES bytes produced by sw_dist_unique_id() on rank 0 and
- * broadcast by the caller.  prob describes this rank's slice of jobs
- * (num_jobs = local count); job_offset/total_jobs place the slice globally.
- * res->plan / planned_rounds receive this rank's rows; scalar results are
- * global and identical on every rank.
+ * Sharded single instance (jobs split across ranks, one process per GPU;
+ * SURVEY.md §8(e), the 10k-job C4 shape).  Replaces the same problem.solve()
+ * crossing as sw_plan_solve, for instances sharded by job.
+ *
+ * Every step of the solve is a pass over the rank's jobs plus one collective:
+ * per-round demand / price-step counts and the makespan are all-reduced, the
+ * deterministic-sum lane partials and the placement keys are all-gathered
+ * (DESIGN.md §7).  Collectives run on RCCL over xGMI (sw_dist_init) or on
+ * caller-supplied host collectives (sw_dist_init_host, e.g. gloo).
+ *
+ * Sharding rule: world must divide 512 (1, 2, 4, … 512) and rank r must hold
+ * exactly the jobs sw_dist_shard_range(total_jobs, world, r) returns.  With
+ * that rule the result (plan rows, counts, objective bits) is identical to
+ * sw_plan_solve on the whole instance, for every world size.
+ *
+ * unique_id points to SW_NCCL_UNIQUE_ID_BYTES bytes produced by
+ * sw_dist_unique_id() on rank 0 and broadcast by the caller.  local describes
+ * this rank's slice of jobs (num_jobs = local count, scalars global);
+ * job_offset/total_jobs place the slice.  res->plan / planned_rounds receive
+ * this rank's rows; scalar results are global and identical on every rank;
+ * res->iters counts collective steps.
  */
 #define SW_NCCL_UNIQUE_ID_BYTES 128
 int sw_dist_unique_id(void* out_bytes);
 int sw_dist_init(sw_handle* h, const void* unique_id, int32_t rank, int32_t world);
 int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset,
                        int64_t total_jobs, sw_result* res);
+int sw_dist_shard_range(int64_t total_jobs, int32_t world, int32_t rank, int64_t* lo,
+                        int64_t* hi);
+
+/*
+ * Host collectives (blocking, in rank order, same call sequence on every
+ * rank).  allgather: recv holds world × bytes, rank r's block at r·bytes.
+ * Each returns 0 on success.
+ */
+typedef struct sw_host_comm {
+    void* ctx;
+    int (*allreduce_sum_i64)(void* ctx, int64_t* buf, int32_t n);
+    int (*allreduce_max_u64)(void* ctx, uint64_t* buf, int32_t n);
+    int (*allreduce_max_f64)(void* ctx, double* buf, int32_t n);
+    int (*allgather)(void* ctx, const void* send, void* recv, int64_t bytes);
+} sw_host_comm;
+/* Sharded mode with host collectives instead of RCCL (the struct is copied;
+ * comm->ctx must outlive the handle's solves). */
+int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int32_t world);
 
 #ifdef __cplusplus
 }

@@ -103,7 +103,7 @@ typedef struct {
  */
 static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
                         int32_t* taken, double* tmp, sel_eval_t* ev) {
-    const int32_t N = P->N, T = P->T;
+    const int32_t N = P->N;
     int64_t Wf = 0, Wall = 0;
     for (int32_t j = 0; j < N; ++j) {
         l[j] = is_inf ? 0 : lforce(P, j, M);
@@ -284,6 +284,19 @@ static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const 
     for (int32_t j = 0; j < N; ++j) placed[j] = 0;
     for (int32_t i = 0; i < A; ++i) placed[ord[i].j] = nin[ord[i].j] - r[i];
     free(ord); free(r); free(ww); free(sel);
+}
+
+/* The packer over plain arrays, for the sharded CPU engine (oracle/shard_twin.c):
+ * pack() reads only N, T, G and the widths. */
+void twin_pack_arrays(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
+                      const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed) {
+    twin_t P;
+    memset(&P, 0, sizeof(P));
+    P.N = N; P.T = T; P.G = G;
+    P.jc = (sw_jobc*)calloc(N > 0 ? (size_t)N : 1, sizeof(sw_jobc));
+    for (int32_t j = 0; j < N; ++j) P.jc[j].w = w[j];
+    pack(&P, nin, k1, k2, y, placed);
+    free(P.jc);
 }
 
 static void build(twin_t* P, const sw_problem* pr) {

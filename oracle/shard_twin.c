@@ -1,0 +1,416 @@
+/*
+ * oracle/shard_twin.c — TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+ *
+ * CPU shard engine for the sharded plan-solve controller
+ * (shockwave-replication_amd/csrc/sw_shard_ctl.h).  One process per rank
+ * holds its slice of jobs (sw_shard_range) as plain host arrays; collectives
+ * go through a caller-supplied sw_host_comm (gloo from Python in
+ * tests/test_shard.py).  It exists so the multi-rank control flow of the
+ * sharded solve — the lane-aligned deterministic sums, the rank-exclusive tie
+ * prefix, the global width-tail arg-max, the gathered placement — is tested on
+ * CPU at world sizes > 1, against the single-instance twin (plan_twin.c):
+ * results must be bit-identical.  The product engine is sw_shard.hip; this
+ * file is never linked into it.
+ *
+ * Per-step semantics follow plan_twin.c's select_level / feasible_level /
+ * levels_between / pack / twin_plan_solve (the reference lines they restate
+ * are cited there: shockwave.py:281-398).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/shockwave_amd.h"
+#include "../shockwave-replication_amd/csrc/sw_arith.h"
+#include "../shockwave-replication_amd/csrc/sw_shard_ctl.h"
+#include "../shockwave-replication_amd/csrc/sw_validate.h"
+
+void twin_pack_arrays(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
+                      const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed);
+
+typedef struct {
+    const sw_host_comm* comm;
+    int32_t rank, world, LW;
+    int64_t N, off, q, P; /* global jobs, slice offset, jobs per lane, padded slice */
+    int32_t NL, T, G, nb;
+    double k, A;
+    const double* beta;
+    const double* ell;
+    const double* p;
+    sw_jobc* jc;
+    int32_t* Tj;
+    float* key; /* [NL][T] */
+    int32_t *l, *taken;
+    int32_t* arr[SW_A_COUNT];
+    uint64_t* y[SW_Y_COUNT];
+    int32_t* w_all;
+    sw_result* res;
+} eng_t;
+
+#define KEY(E, i, n) ((E)->key[(size_t)(i) * (E)->T + (n)])
+
+static double fv(const eng_t* E, int32_t i, int32_t n) {
+    return sw_f(&E->jc[i], n, E->nb, E->beta, E->ell);
+}
+
+static int32_t lforce(const eng_t* E, int32_t i, double M) {
+    int32_t c = 0;
+    for (int32_t n = 0; n < E->Tj[i]; ++n) c += (sw_g(&E->jc[i], n) > M);
+    return c;
+}
+
+static int32_t cnt(const eng_t* E, int32_t i, uint32_t rho, int ge) {
+    int32_t c = 0;
+    for (int32_t n = E->l[i]; n < E->Tj[i]; ++n) {
+        uint32_t b = sw_fbits_of(KEY(E, i, n));
+        c += ge ? (b >= rho) : (b > rho);
+    }
+    return c;
+}
+
+/* lane partials of v over this rank's lanes, gathered into out[SW_DET_LANES] */
+static int lanes_gather(eng_t* E, const double* v, double* out) {
+    double* mine = (double*)calloc((size_t)E->LW, sizeof(double));
+    if (!mine) return -1;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int64_t L = (E->off + i) / E->q - (int64_t)E->rank * E->LW;
+        mine[L] = mine[L] + v[i];
+    }
+    int rc = E->comm->allgather(E->comm->ctx, mine, out, (int64_t)E->LW * (int64_t)sizeof(double));
+    free(mine);
+    return rc;
+}
+
+static int e_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
+    eng_t* E = (eng_t*)ctx;
+    double mx[2] = {0.0, 0.0};
+    for (int32_t i = 0; i < E->NL; ++i) mx[0] = sw_max(mx[0], E->jc[i].a);
+    if (E->comm->allreduce_max_f64(E->comm->ctx, mx, 1)) return -1;
+    E->A = mx[0];
+    for (int32_t i = 0; i < E->NL; ++i) {
+        double prev = fv(E, i, 0), vm = 0.0;
+        for (int32_t n = 0; n < E->T; ++n) {
+            double cur = fv(E, i, n + 1);
+            double v = sw_pos(cur - prev);
+            vm = (n == 0) ? v : sw_min(vm, v);
+            KEY(E, i, n) = sw_key(vm, E->jc[i].w, E->A);
+            prev = cur;
+        }
+        mx[1] = sw_max(mx[1], sw_g(&E->jc[i], E->Tj[i]));
+    }
+    if (E->comm->allreduce_max_f64(E->comm->ctx, mx + 1, 1)) return -1;
+    *A = E->A;
+    *lb = mx[1];
+    /* widths of every job, gathered in padded per-rank blocks */
+    int32_t* blk = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1), sizeof(int32_t));
+    int32_t* all = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1) * E->world, sizeof(int32_t));
+    if (!blk || !all) { free(blk); free(all); return -1; }
+    for (int32_t i = 0; i < E->NL; ++i) blk[i] = E->jc[i].w;
+    int rc = E->comm->allgather(E->comm->ctx, blk, all, E->P * (int64_t)sizeof(int32_t));
+    /* rank r's block starts at r·P, which is also its first global job */
+    for (int64_t j = 0; j < E->N; ++j) {
+        w_all[j] = all[j];
+        E->w_all[j] = all[j];
+    }
+    free(blk); free(all);
+    return rc;
+}
+
+static int e_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
+    eng_t* E = (eng_t*)ctx;
+    out[0] = out[1] = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        E->l[i] = is_inf ? 0 : lforce(E, i, M);
+        out[0] += (int64_t)E->jc[i].w * E->l[i];
+        out[1] += (int64_t)E->jc[i].w * (E->Tj[i] - E->l[i]);
+    }
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, 2);
+}
+
+static int e_count_gt(void* ctx, const uint32_t* rho, int32_t K, int64_t* out) {
+    eng_t* E = (eng_t*)ctx;
+    for (int32_t k = 0; k < K; ++k) {
+        out[k] = 0;
+        for (int32_t i = 0; i < E->NL; ++i) out[k] += (int64_t)E->jc[i].w * cnt(E, i, rho[k], 0);
+    }
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K);
+}
+
+static int e_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
+    eng_t* E = (eng_t*)ctx;
+    for (int32_t k = 0; k < K; ++k) {
+        out[k] = 0;
+        for (int32_t i = 0; i < E->NL; ++i) out[k] += (int64_t)E->jc[i].w * lforce(E, i, M[k]);
+    }
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K);
+}
+
+static int e_between(void* ctx, double a, double b, int64_t* out) {
+    eng_t* E = (eng_t*)ctx;
+    int64_t c = 0;
+    for (int32_t i = 0; i < E->NL; ++i)
+        for (int32_t n = 0; n <= E->Tj[i]; ++n) {
+            double v = sw_g(&E->jc[i], n);
+            c += (v > a && v < b);
+        }
+    *out = c;
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, 1);
+}
+
+static int e_take_all(void* ctx) {
+    eng_t* E = (eng_t*)ctx;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        E->arr[SW_A_N][i] = E->Tj[i];
+        E->taken[i] = E->Tj[i] - E->l[i];
+    }
+    return 0;
+}
+
+static int e_take(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl) {
+    eng_t* E = (eng_t*)ctx;
+    int64_t mine[2] = {0, 0};
+    for (int32_t i = 0; i < E->NL; ++i) {
+        E->taken[i] = cnt(E, i, rho, 0);
+        mine[0] += (int64_t)E->jc[i].w * E->taken[i];
+        mine[1] += (int64_t)E->jc[i].w * (cnt(E, i, rho, 1) - E->taken[i]);
+    }
+    int64_t* all = (int64_t*)malloc(sizeof(int64_t) * 2 * E->world);
+    if (!all) return -1;
+    int rc = E->comm->allgather(E->comm->ctx, mine, all, 2 * (int64_t)sizeof(int64_t));
+    *wt = 0;
+    *excl = 0;
+    for (int32_t r = 0; r < E->world; ++r) {
+        *wt += all[2 * r];
+        if (r < E->rank) *excl += all[2 * r + 1];
+    }
+    free(all);
+    return rc;
+}
+
+static int e_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used) {
+    eng_t* E = (eng_t*)ctx;
+    int64_t u = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int32_t tie = cnt(E, i, rho, 1) - E->taken[i];
+        const int64_t wj = E->jc[i].w;
+        int32_t tt;
+        if (excl + wj * tie <= rem) tt = tie;
+        else if (excl <= rem) tt = (int32_t)((rem - excl) / wj);
+        else tt = 0;
+        E->arr[SW_A_N][i] = E->l[i] + E->taken[i] + tt;
+        u += wj * tt;
+        excl += wj * tie;
+    }
+    *used = u;
+    return E->comm->allreduce_sum_i64(E->comm->ctx, used, 1);
+}
+
+static int e_tail_best(void* ctx, int64_t rem2, uint64_t* best) {
+    eng_t* E = (eng_t*)ctx;
+    uint64_t b = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int32_t n = E->arr[SW_A_N][i];
+        if (n < E->Tj[i] && (int64_t)E->jc[i].w <= rem2) {
+            const uint64_t kk = ((uint64_t)sw_fbits_of(KEY(E, i, n)) << 32) |
+                                (uint64_t)(0xFFFFFFFFu - (uint32_t)(E->off + i));
+            b = kk > b ? kk : b;
+        }
+    }
+    *best = b;
+    return E->comm->allreduce_max_u64(E->comm->ctx, best, 1);
+}
+
+static int e_tail_apply(void* ctx, int64_t jb) {
+    eng_t* E = (eng_t*)ctx;
+    if (jb >= E->off && jb < E->off + E->NL) E->arr[SW_A_N][jb - E->off] += 1;
+    return 0;
+}
+
+static int e_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
+                  int64_t* isum) {
+    eng_t* E = (eng_t*)ctx;
+    const int32_t NL = E->NL;
+    double* va = (double*)calloc((size_t)(NL > 0 ? NL : 1), sizeof(double));
+    double* vb = (double*)calloc((size_t)(NL > 0 ? NL : 1), sizeof(double));
+    if (!va || !vb) { free(va); free(vb); return -1; }
+    double g = 0.0;
+    int64_t s = 0;
+    for (int32_t i = 0; i < NL; ++i) {
+        const sw_jobc* c = &E->jc[i];
+        if (sel == SW_EV_SELECT) {
+            const int32_t n = E->arr[SW_A_N][i];
+            va[i] = fv(E, i, n);
+            vb[i] = fv(E, i, E->l[i] + E->taken[i]);
+            g = sw_max(g, sw_g(c, n));
+        } else if (sel == SW_EV_GMAX) {
+            g = sw_max(g, sw_g(c, E->arr[arg][i]));
+        } else if (sel == SW_EV_PACKED) {
+            const int32_t pl = E->arr[arg][i];
+            va[i] = fv(E, i, pl);
+            g = sw_max(g, sw_g(c, pl));
+            s += (int64_t)c->w * (E->arr[SW_A_NB][i] - pl);
+        } else if (sel == SW_EV_P2OK) {
+            s += E->arr[SW_A_PL][i] != E->arr[SW_A_NFIN][i];
+        } else { /* SW_EV_FINAL */
+            const uint64_t m = E->y[arg][i];
+            int32_t cn = 0;
+            int64_t S = 0;
+            for (int32_t t = 0; t < E->T; ++t)
+                if ((m >> t) & 1u) { cn += 1; S += t; }
+            va[i] = fv(E, i, cn);
+            vb[i] = cn > 0 ? ((double)S / (double)cn) * E->p[i] : 0.0;
+            g = sw_max(g, sw_g(c, cn));
+            s += cn > 0;
+            if (E->res->plan)
+                for (int32_t t = 0; t < E->T; ++t)
+                    E->res->plan[(size_t)i * E->T + t] = (uint8_t)((m >> t) & 1u);
+            if (E->res->planned_rounds) E->res->planned_rounds[i] = cn;
+        }
+    }
+    int rc = lanes_gather(E, va, lanesA);
+    if (!rc) rc = lanes_gather(E, vb, lanesB);
+    *gm = g;
+    *isum = s;
+    if (!rc) rc = E->comm->allreduce_max_f64(E->comm->ctx, gm, 1);
+    if (!rc) rc = E->comm->allreduce_sum_i64(E->comm->ctx, isum, 1);
+    free(va); free(vb);
+    return rc;
+}
+
+static int e_copy(void* ctx, int32_t dst, int32_t src) {
+    eng_t* E = (eng_t*)ctx;
+    if (E->NL) memcpy(E->arr[dst], E->arr[src], sizeof(int32_t) * (size_t)E->NL);
+    return 0;
+}
+
+static int e_copy_y(void* ctx, int32_t dst, int32_t src) {
+    eng_t* E = (eng_t*)ctx;
+    if (E->NL) memcpy(E->y[dst], E->y[src], sizeof(uint64_t) * (size_t)E->NL);
+    return 0;
+}
+
+/* gathered placement: every rank runs the twin's packer on all jobs */
+typedef struct {
+    uint64_t k1;
+    uint32_t k2;
+    int32_t nin;
+} pk_t;
+
+static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
+    eng_t* E = (eng_t*)ctx;
+    const int64_t P = E->P > 0 ? E->P : 1, N = E->N;
+    pk_t* mine = (pk_t*)calloc((size_t)P, sizeof(pk_t));
+    pk_t* all = (pk_t*)calloc((size_t)P * E->world, sizeof(pk_t));
+    int32_t* nin = (int32_t*)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+    uint64_t* k1 = (uint64_t*)calloc((size_t)(N > 0 ? N : 1), sizeof(uint64_t));
+    uint32_t* k2 = (uint32_t*)calloc((size_t)(N > 0 ? N : 1), sizeof(uint32_t));
+    int32_t* placed = (int32_t*)calloc((size_t)(N > 0 ? N : 1), sizeof(int32_t));
+    uint8_t* y = (uint8_t*)calloc((size_t)(N > 0 ? N : 1) * E->T, 1);
+    int rc = -1;
+    if (!mine || !all || !nin || !k1 || !k2 || !placed || !y) goto out;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int32_t n = E->arr[src][i];
+        mine[i].nin = n;
+        if (n > 0) {
+            if (mode != 2) {
+                const double lvl = sw_g(&E->jc[i], n - 1);
+                const int crit = E->k > 0.0 && lvl > Mb;
+                mine[i].k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)E->jc[i].w : 0);
+                mine[i].k2 = sw_fbits_of(KEY(E, i, n - 1));
+            } else {
+                mine[i].k1 = sw_bits(E->p[i] / (double)n);
+                mine[i].k2 = 0;
+            }
+        }
+    }
+    rc = E->comm->allgather(E->comm->ctx, mine, all, P * (int64_t)sizeof(pk_t));
+    if (rc) goto out;
+    for (int64_t j = 0; j < N; ++j) {
+        nin[j] = all[j].nin; /* blocks are P long and contiguous: job j at j */
+        k1[j] = all[j].k1;
+        k2[j] = all[j].k2;
+    }
+    twin_pack_arrays((int32_t)N, E->T, E->G, E->w_all, nin, k1, k2, y, placed);
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int64_t j = E->off + i;
+        uint64_t m = 0;
+        for (int32_t t = 0; t < E->T; ++t) m |= (uint64_t)y[(size_t)j * E->T + t] << t;
+        E->y[ydst][i] = m;
+        E->arr[pdst][i] = placed[j];
+    }
+out:
+    free(mine); free(all); free(nin); free(k1); free(k2); free(placed); free(y);
+    return rc;
+}
+
+/*
+ * One rank's sharded solve (same contract as sw_dist_plan_solve): `local`
+ * holds this rank's jobs, [job_offset, job_offset + local->num_jobs) of
+ * total_jobs, which must be sw_shard_range(total_jobs, world, rank).
+ */
+int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, const sw_problem* local,
+                     int64_t job_offset, int64_t total_jobs, sw_result* res) {
+    int64_t lo, hi;
+    if (sw_validate_problem(local) != 0) return SW_ERR_INVALID;
+    if (sw_shard_range(total_jobs, world, rank, &lo, &hi) != 0) return SW_ERR_INVALID;
+    if (lo != job_offset || hi - lo != local->num_jobs) return SW_ERR_INVALID;
+    eng_t E;
+    memset(&E, 0, sizeof(E));
+    E.comm = comm;
+    E.rank = rank;
+    E.world = world;
+    E.LW = SW_DET_LANES / world;
+    E.N = total_jobs;
+    E.off = job_offset;
+    E.q = (total_jobs + SW_DET_LANES - 1) / SW_DET_LANES;
+    if (E.q == 0) E.q = 1;
+    E.P = (int64_t)E.LW * E.q;
+    E.NL = local->num_jobs;
+    E.T = local->future_rounds;
+    E.G = local->num_gpus;
+    E.nb = local->num_bases;
+    E.k = local->regularizer;
+    E.beta = local->bases;
+    E.ell = local->log_bases;
+    E.p = local->priority;
+    E.res = res;
+    const size_t NN = E.NL > 0 ? (size_t)E.NL : 1;
+    E.jc = (sw_jobc*)malloc(sizeof(sw_jobc) * NN);
+    E.Tj = (int32_t*)malloc(sizeof(int32_t) * NN);
+    E.key = (float*)malloc(sizeof(float) * NN * E.T);
+    E.l = (int32_t*)calloc(NN, sizeof(int32_t));
+    E.taken = (int32_t*)calloc(NN, sizeof(int32_t));
+    for (int a = 0; a < SW_A_COUNT; ++a) E.arr[a] = (int32_t*)calloc(NN, sizeof(int32_t));
+    for (int a = 0; a < SW_Y_COUNT; ++a) E.y[a] = (uint64_t*)calloc(NN, sizeof(uint64_t));
+    E.w_all = (int32_t*)calloc(total_jobs > 0 ? (size_t)total_jobs : 1, sizeof(int32_t));
+    for (int32_t i = 0; i < E.NL; ++i) {
+        E.jc[i] = sw_make_jobc((int32_t)total_jobs, E.T, local->round_duration, local->nworkers[i],
+                               local->epoch_duration[i], local->completed_epochs[i],
+                               local->total_epochs[i], local->remaining_runtime[i],
+                               local->priority[i]);
+        E.Tj[i] = local->nworkers[i] <= E.G ? E.T : 0;
+    }
+    sw_shard_ops ops;
+    ops.ctx = &E;
+    ops.setup = e_setup;
+    ops.force = e_force;
+    ops.count_gt = e_count_gt;
+    ops.feasible = e_feasible;
+    ops.between = e_between;
+    ops.take_all = e_take_all;
+    ops.take = e_take;
+    ops.assign = e_assign;
+    ops.tail_best = e_tail_best;
+    ops.tail_apply = e_tail_apply;
+    ops.eval = e_eval;
+    ops.copy = e_copy;
+    ops.copy_y = e_copy_y;
+    ops.pack = e_pack;
+    int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
+                            &res->makespan, &res->p2_objective, &res->bound, &res->iters,
+                            &res->status);
+    free(E.jc); free(E.Tj); free(E.key); free(E.l); free(E.taken); free(E.w_all);
+    for (int a = 0; a < SW_A_COUNT; ++a) free(E.arr[a]);
+    for (int a = 0; a < SW_Y_COUNT; ++a) free(E.y[a]);
+    return rc < 0 ? SW_ERR_RCCL : rc;
+}

@@ -1,0 +1,99 @@
+/*
+ * sw_handle.h — the opaque sw_handle of include/shockwave_amd.h (private to
+ * the library: sw_api.hip, sw_shard.hip) and small RAII-free buffer helpers.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/shockwave_amd.h"
+#include "sw_device.h"
+
+struct sw_shard_state;
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;  // elements
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+template <typename T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct sw_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    /* batch description (host) */
+    int32_t count = 0;
+    int64_t total_jobs = 0;
+    int64_t total_plan = 0;
+    int32_t maxN = 0, maxT = 0;
+    std::vector<sw_inst_dev> inst;
+    std::vector<int32_t> Ns, Ts;
+    /* device */
+    DevBuf<sw_inst_dev> d_inst;
+    DevBuf<int32_t> d_w, d_F, d_E, d_planned;
+    DevBuf<double> d_d, d_R, d_p;
+    DevBuf<uint8_t> d_plan, d_ws_u8;
+    DevBuf<uint64_t> d_ws_u64, d_ws_sort;
+    DevBuf<float> d_ws_keys;
+    DevBuf<sw_jobc> d_ws_jc;
+    DevBuf<sw_out_dev> d_out;
+    DevBuf<uint64_t> d_stamps; /* SW_STAMPS diagnostic builds */
+    /* pinned staging */
+    HostBuf<int32_t> h_w, h_F, h_E, h_planned;
+    HostBuf<double> h_d, h_R, h_p;
+    HostBuf<uint8_t> h_plan;
+    HostBuf<sw_out_dev> h_out;
+    /* timing: one event pair per timed launch, collected lazily */
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0; /* pairs recorded and not yet collected */
+    double ms_plan = 0.0;
+    int32_t runs = 0;
+    /* sharded mode (sw_shard.hip) */
+    sw_shard_state* shard = nullptr;
+};
+
+/* sw_shard.hip: frees the sharded-mode state and communicator */
+void sw_shard_release(sw_handle* h);
+

@@ -32,6 +32,7 @@
 #include "sw_arith.h"
 #include "sw_block.h"
 #include "sw_device.h"
+#include "sw_pack.h"
 
 namespace {
 
@@ -86,6 +87,7 @@ struct Ctx {
     int32_t* pord;
     uint64_t* sbuf; /* ONE: [2][2][1024] bitonic exchange; else [2][NP] keys */
     int32_t *H, *SH;
+    sw_pack_lds* PL;
     int64_t* misc;
     /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
     sw_jobc jcs[SW_JPT];
@@ -590,7 +592,7 @@ struct Ctx {
                 jp[s] = (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
                 st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | ((uint32_t)w_in[jp[s]] << 8)) : 0u;
             }
-            rounds_block(A_, st, mk);
+            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk);
             for_jobs([&](int j, int s) { (void)s; placed_out[j] = 0; });
             __syncthreads();
 #pragma unroll
@@ -647,119 +649,6 @@ struct Ctx {
      * lane-major); their state lives at tslot(p). */
     __device__ __forceinline__ void rounds(int A_, int PPL) {
         rounds_mem(A_, PPL);
-    }
-
-    /* ONE: all waves; thread t keeps its positions E·t … E·t+E−1 (as left
-     * by the sort) in VGPRs.  Block scans/sums take one barrier each; the
-     * histograms H/SH are double-buffered by round parity. */
-    __device__ __forceinline__ void rounds_block(int A_, uint32_t (&st)[SW_JPT],
-                                                 uint64_t (&mk)[SW_JPT]) {
-        constexpr int E = SW_JPT;
-        const int tid = threadIdx.x;
-        const int lane = lane_id();
-        int32_t* Hb[2] = {H, H + 68};
-        int32_t* SHb[2] = {SH, SH + 68};
-        if (tid < 65) { Hb[0][tid] = 0; SHb[0][tid] = 0; }
-        __syncthreads();
-        for (int t = 0; t < T; ++t) {
-            const int R = T - t;
-            int32_t* Hc = Hb[t & 1];
-            int32_t* SHc = SHb[t & 1];
-            int32_t cap = G;
-#pragma unroll
-            for (int i = 0; i < E; ++i) {
-                if (E * tid + i < A_) {
-                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
-                    atomicAdd(&Hc[rr], (int32_t)st_w(st[i]));
-                }
-            }
-            /* clear next round's buffers (read by nobody this round) */
-            if (tid < 65) { Hb[(t + 1) & 1][tid] = 0; SHb[(t + 1) & 1][tid] = 0; }
-            __syncthreads();
-            /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
-            const int32_t hv = (lane + 1 <= R) ? Hc[lane + 1] : 0;
-            const int32_t S0 = wave_sufscan_i32(hv);
-            const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-            const int32_t need = (lane < R) ? (S1 - lane * S0) - G * (R - 1 - lane) : -1;
-            int mstart = R - 1;
-            while (mstart >= 0) {
-                const int32_t shv = (lane + 1 <= R) ? SHc[lane + 1] : 0;
-                const int32_t red = wave_sufscan_i32(shv);
-                const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
-                if (mask == 0) break;
-                const int m = 63 - __builtin_clzll(mask);
-                const int32_t q = __shfl(need - red, m, 64);
-                int32_t lt = 0;
-#pragma unroll
-                for (int i = 0; i < E; ++i) {
-                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
-                    if (E * tid + i < A_ && !st_sel(st[i]) && rr > m) lt += (int32_t)st_w(st[i]);
-                }
-                int32_t tot;
-                int32_t ex = blk.exscan(lt, tot);
-                int32_t took = 0;
-#pragma unroll
-                for (int i = 0; i < E; ++i) {
-                    const int rr = (int)st_r(st[i]) < R ? (int)st_r(st[i]) : R;
-                    if (E * tid + i < A_ && !st_sel(st[i]) && rr > m) {
-                        const int32_t w = (int32_t)st_w(st[i]);
-                        if (ex < q && ex + w <= cap) {
-                            st[i] |= (1u << 16);
-                            atomicAdd(&SHc[rr], w);
-                            took += w;
-                        }
-                        ex += w;
-                    }
-                }
-                cap -= blk.sum32(took);
-                mstart = m - 1;
-            }
-            {
-                int32_t lt = 0;
-#pragma unroll
-                for (int i = 0; i < E; ++i)
-                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) lt += (int32_t)st_w(st[i]);
-                int32_t tot;
-                int32_t ex = blk.exscan(lt, tot);
-                int32_t took = 0;
-#pragma unroll
-                for (int i = 0; i < E; ++i) {
-                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0) {
-                        const int32_t w = (int32_t)st_w(st[i]);
-                        if (ex + w <= cap) { st[i] |= (1u << 16); took += w; }
-                        ex += w;
-                    }
-                }
-                cap -= blk.sum32(took);
-            }
-            /* width tail: first position in order that still fits; the key
-             * carries (position << 4 | w) so the min also names the width */
-            while (cap > 0) {
-                int32_t best = 0x7FFFFFFF;
-#pragma unroll
-                for (int i = E - 1; i >= 0; --i) {
-                    if (E * tid + i < A_ && !st_sel(st[i]) && st_r(st[i]) > 0 && (int32_t)st_w(st[i]) <= cap)
-                        best = ((E * tid + i) << 4) | (int32_t)st_w(st[i]);
-                }
-                best = blk.min32(best);
-                if (best == 0x7FFFFFFF) break;
-                const int pos = best >> 4;
-                if (pos / E == tid) {
-#pragma unroll
-                    for (int i = 0; i < E; ++i)
-                        if (i == pos % E) st[i] |= (1u << 16);
-                }
-                cap -= best & 15;
-            }
-#pragma unroll
-            for (int i = 0; i < E; ++i) {
-                if (E * tid + i < A_ && st_sel(st[i])) {
-                    mk[i] |= (1ull << t);
-                    st[i] = (st[i] & 0xFF00u) | (st_r(st[i]) - 1u);
-                }
-            }
-        }
-        __syncthreads();
     }
 
     /* !ONE: the same loop over position state in the HBM workspace. */
@@ -906,8 +795,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     double* bt = (double*)carve(sizeof(double) * 2 * SW_BMAX);
     c.beta = bt;
     c.ell = bt + SW_BMAX;
-    c.H = (int32_t*)carve(sizeof(int32_t) * 136);
-    c.SH = (int32_t*)carve(sizeof(int32_t) * 136);
+    c.PL = (sw_pack_lds*)carve(sizeof(sw_pack_lds));
+    c.H = c.PL->H[0];
+    c.SH = c.PL->SH[0];
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
     if (threadIdx.x < SW_BMAX) {
         bt[threadIdx.x] = I->beta[threadIdx.x];
@@ -1096,7 +986,7 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
 extern "C" size_t sw_plan_kernel_lds_bytes(int one) {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     size_t s = r16(sizeof(sw_xchg)) + r16(sizeof(double) * 2 * SW_BMAX) +
-               2 * r16(sizeof(int32_t) * 136) + r16(sizeof(int64_t) * 8);
+               r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8);
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
         s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);

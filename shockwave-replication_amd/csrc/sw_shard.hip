@@ -1,0 +1,942 @@
+/*
+ * sw_shard.hip — sharded single-instance plan solve on MI355X
+ * (include/shockwave_amd.h sw_dist_*).
+ *
+ * One process per GPU holds a contiguous slice of the jobs (sw_shard_range).
+ * The controller (sw_shard_ctl.h, the algorithm of oracle/plan_twin.c as a
+ * sequence of steps) runs on the host of every rank; this file is its GPU
+ * engine.  Each step is
+ *      one or two kernels over the rank's jobs in HBM
+ *   →  one collective on the handle's stream (RCCL over xGMI, or host
+ *      callbacks)
+ *   →  a few bytes back to the host (pinned), one stream sync.
+ * The placement steps never come back to the host: local keys → all-gather
+ * → all-pairs rank sort → block-wide round loop, all on the stream.
+ *
+ * Layout in HBM (per rank, NL local jobs, T rounds):
+ *   jc[NL] (sw_jobc, 64 B)   keys[NL][T] fp32   l, taken, 5 count arrays [NL] i32
+ *   3 round-bitmask arrays [NL] u64   plan[NL][T] u8   planned[NL] i32
+ *   red[128] i64 (step results)   exchange blocks for the gathers
+ *   placement: send[P] / all[W·P] entries (24 B), rank[W·P], order[W·P]
+ *
+ * Kernels and what bounds them (all latency-bound at C4's 1,250 jobs per
+ * rank; DESIGN.md §7 has the per-step budget):
+ *   k_force / k_take / k_between / k_tail_best   thread per job, binary
+ *        searches on the monotone g and key rows, wave reductions + atomics
+ *   k_count / k_feasible   thread per (job, round) element: one binary
+ *        search over the ≤63 sorted thresholds, an LDS histogram, a suffix
+ *        sum on the host — K price/level probes per pass (K-ary search)
+ *   k_assign   one workgroup: the job-ordered tie group as a block scan
+ *   k_eval     one workgroup, thread per deterministic-sum lane (sw_detsum's
+ *        left-to-right chunks), so the gathered lanes reproduce the
+ *        single-instance sums bit for bit
+ *   k_pack_rank / k_pack_rounds   the placement (sw_pack.h)
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/shockwave_amd.h"
+#include "sw_arith.h"
+#include "sw_block.h"
+#include "sw_device.h"
+#include "sw_handle.h"
+#include "sw_pack.h"
+#include "sw_shard_ctl.h"
+#include "sw_validate.h"
+
+namespace {
+
+constexpr int kTB = 256;  /* threads per block of the per-job kernels */
+constexpr int kRed = 128; /* entries of the step-result buffer        */
+
+struct sw_pack_ent {
+    uint64_t khi, klo; /* order key (desc); klo low 32 bits = ~job */
+    uint32_t st;       /* rounds | width << 8 (0 = not placed)      */
+    uint32_t pad;
+};
+
+/* kernel view of one rank's shard (passed by value) */
+struct ShardDev {
+    int32_t NL, T, G, nb, LW, rank;
+    int64_t off, N, q, P;
+    double k;
+    double beta[SW_BMAX], ell[SW_BMAX];
+    const sw_jobc* jc;
+    float* keys;
+    const double* p;
+    int32_t* l;
+    int32_t* taken;
+    int32_t* arr[SW_A_COUNT];
+    uint64_t* y[SW_Y_COUNT];
+    uint8_t* plan;
+    int32_t* planned;
+    long long* red; /* i64 / u64-bit step results */
+};
+
+struct Thresholds {
+    uint64_t v[SW_SHARD_K]; /* u32 key bits or fp64 bits, ascending */
+    int32_t K;
+};
+
+__device__ __forceinline__ int tj_of(const ShardDev& S, const sw_jobc& c) { return c.w <= S.G ? S.T : 0; }
+
+__device__ __forceinline__ int g_count_gt(const sw_jobc& c, int hi, double x) {
+    int lo = 0;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sw_g(&c, mid) > x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int g_count_ge(const sw_jobc& c, int hi, double x) {
+    int lo = 0;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sw_g(&c, mid) >= x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+/* #{n ∈ [l, tj) : key(n) > ρ (≥ ρ)} — keys are nonincreasing along the row */
+template <bool GE>
+__device__ __forceinline__ int key_count(const float* row, int l, int tj, uint32_t rho) {
+    int lo = l, hi = tj;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t b = sw_fbits_of(row[mid]);
+        if (GE ? (b >= rho) : (b > rho)) lo = mid + 1; else hi = mid;
+    }
+    return lo - l;
+}
+
+__device__ __forceinline__ void red_add(long long* dst, long long v) {
+    v = wave_sum(v);
+    if (lane_id() == 0 && v != 0) atomicAdd((unsigned long long*)dst, (unsigned long long)v);
+}
+__device__ __forceinline__ void red_umax(long long* dst, uint64_t v) {
+    v = wave_max(v);
+    if (lane_id() == 0 && v != 0) atomicMax((unsigned long long*)dst, (unsigned long long)v);
+}
+
+/* ---- setup ---------------------------------------------------------------- */
+
+__global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const int32_t* w,
+                                               const double* d, const int32_t* F,
+                                               const int32_t* E, const double* R, double delta) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t amax = 0, lb = 0;
+    if (i < S.NL) {
+        const sw_jobc c = sw_make_jobc((int32_t)S.N, S.T, delta, w[i], d[i], F[i], E[i], R[i], S.p[i]);
+        jc[i] = c;
+        amax = sw_bits(c.a); /* a, g ≥ 0: bit order = value order */
+        lb = sw_bits(sw_g(&c, tj_of(S, c)));
+    }
+    red_umax(S.red + 0, amax);
+    red_umax(S.red + 1, lb);
+}
+
+/* key rows (twin: build), A read from the all-reduced step result */
+__global__ __launch_bounds__(kTB) void k_keys(ShardDev S) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.NL) return;
+    const double A = sw_from_bits((uint64_t)S.red[0]);
+    const sw_jobc c = S.jc[i];
+    float* row = S.keys + (size_t)i * S.T;
+    double prev = sw_f(&c, 0, S.nb, S.beta, S.ell), vm = 0.0;
+    for (int n = 0; n < S.T; ++n) {
+        const double cur = sw_f(&c, n + 1, S.nb, S.beta, S.ell);
+        const double v = sw_pos(cur - prev);
+        vm = (n == 0) ? v : sw_min(vm, v);
+        row[n] = sw_key(vm, c.w, A);
+        prev = cur;
+    }
+}
+
+/* ---- SELECT steps ----------------------------------------------------------- */
+
+__global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    long long wf = 0, wall = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int tj = tj_of(S, c);
+        const int l = is_inf ? 0 : g_count_gt(c, tj, M);
+        S.l[i] = l;
+        wf = (long long)c.w * l;
+        wall = (long long)c.w * (tj - l);
+    }
+    red_add(S.red + 0, wf);
+    red_add(S.red + 1, wall);
+}
+
+/* K probes at once: element (job, n) adds w to bin #{m : thr_m < v}; the
+ * count for probe m is the suffix Σ_{b > m} bin[b] (host side). */
+template <bool LEVEL>
+__global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
+    __shared__ int32_t bins[SW_SHARD_K + 1];
+    __shared__ uint64_t thr[SW_SHARD_K];
+    if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
+    if (threadIdx.x < th.K) thr[threadIdx.x] = th.v[threadIdx.x];
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (e < (int64_t)S.NL * S.T) {
+        const int i = (int)(e / S.T), n = (int)(e % S.T);
+        const sw_jobc c = S.jc[i];
+        const int tj = tj_of(S, c);
+        bool live;
+        int lo = 0, hi = th.K;
+        if (LEVEL) {
+            live = n < tj;
+            if (live) {
+                const double v = sw_g(&c, n);
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sw_from_bits(thr[mid]) < v) lo = mid + 1; else hi = mid;
+                }
+            }
+        } else {
+            live = n >= S.l[i] && n < tj;
+            if (live) {
+                const uint32_t b = sw_fbits_of(S.keys[(size_t)i * S.T + n]);
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if ((uint32_t)thr[mid] < b) lo = mid + 1; else hi = mid;
+                }
+            }
+        }
+        if (live && lo > 0) atomicAdd(&bins[lo], c.w);
+    }
+    __syncthreads();
+    if (threadIdx.x <= th.K && threadIdx.x > 0 && bins[threadIdx.x] != 0)
+        atomicAdd((unsigned long long*)(S.red + threadIdx.x), (unsigned long long)bins[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    long long cnt = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int n1 = tj_of(S, c) + 1;
+        const int d = g_count_gt(c, n1, a) - g_count_ge(c, n1, b);
+        cnt = d > 0 ? d : 0;
+    }
+    red_add(S.red + 0, cnt);
+}
+
+__global__ __launch_bounds__(kTB) void k_take_all(ShardDev S) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.NL) return;
+    const int tj = tj_of(S, S.jc[i]);
+    S.arr[SW_A_N][i] = tj;
+    S.taken[i] = tj - S.l[i];
+}
+
+__global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    long long wt = 0, tie = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int tj = tj_of(S, c), l = S.l[i];
+        const float* row = S.keys + (size_t)i * S.T;
+        const int tk = key_count<false>(row, l, tj, rho);
+        S.taken[i] = tk;
+        wt = (long long)c.w * tk;
+        tie = (long long)c.w * (key_count<true>(row, l, tj, rho) - tk);
+    }
+    red_add(S.red + 0, wt);
+    red_add(S.red + 1, tie);
+}
+
+/* tie group in job order: one workgroup, thread t owns a contiguous chunk */
+__global__ __launch_bounds__(SW_BLOCK) void k_assign(ShardDev S, uint32_t rho, long long rem,
+                                                     long long excl0) {
+    __shared__ long long wsum[SW_WAVES];
+    const int tid = threadIdx.x;
+    const int per = (S.NL + SW_BLOCK - 1) / SW_BLOCK;
+    const int lo = tid * per, hi = min(S.NL, lo + per);
+    long long mine = 0;
+    for (int i = lo; i < hi; ++i) {
+        const sw_jobc c = S.jc[i];
+        const int tie = key_count<true>(S.keys + (size_t)i * S.T, S.l[i], tj_of(S, c), rho) - S.taken[i];
+        mine += (long long)c.w * tie;
+    }
+    const long long inc = wave_incscan(mine);
+    if (lane_id() == 63) wsum[wave_id()] = inc;
+    __syncthreads();
+    long long base = excl0;
+    for (int w = 0; w < wave_id(); ++w) base += wsum[w];
+    long long excl = base + inc - mine, used = 0;
+    for (int i = lo; i < hi; ++i) {
+        const sw_jobc c = S.jc[i];
+        const int tie = key_count<true>(S.keys + (size_t)i * S.T, S.l[i], tj_of(S, c), rho) - S.taken[i];
+        const long long wj = c.w;
+        int tt;
+        if (excl + wj * tie <= rem) tt = tie;
+        else if (excl <= rem) tt = (int)((rem - excl) / wj);
+        else tt = 0;
+        S.arr[SW_A_N][i] = S.l[i] + S.taken[i] + tt;
+        used += wj * tt;
+        excl += wj * tie;
+    }
+    red_add(S.red + 0, used);
+}
+
+__global__ __launch_bounds__(kTB) void k_tail_best(ShardDev S, long long rem2) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t best = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int n = S.arr[SW_A_N][i];
+        if (n < tj_of(S, c) && (long long)c.w <= rem2)
+            best = ((uint64_t)sw_fbits_of(S.keys[(size_t)i * S.T + n]) << 32) |
+                   (uint64_t)(0xFFFFFFFFu - (uint32_t)(S.off + i));
+    }
+    red_umax(S.red + 0, best);
+}
+
+__global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
+
+/* ---- reductions with deterministic lane sums ------------------------------- */
+
+/* Thread ℓ < LW owns deterministic-sum lane rank·LW + ℓ (jobs [L·q, L·q+q)).
+ * Writes [A lanes][B lanes][gm bits][isum] to out. */
+__global__ __launch_bounds__(SW_BLOCK) void k_eval(ShardDev S, int sel, int arg, double* out) {
+    __shared__ uint64_t sg[SW_WAVES];
+    __shared__ long long ss[SW_WAVES];
+    const int lane = threadIdx.x;
+    double fa = 0.0, fb = 0.0, gm = 0.0;
+    long long is = 0;
+    if (lane < S.LW) {
+        const int64_t L = (int64_t)S.rank * S.LW + lane;
+        const int64_t j0 = L * S.q, j1 = min(S.N, j0 + S.q);
+        for (int64_t j = j0; j < j1; ++j) {
+            const int i = (int)(j - S.off);
+            const sw_jobc c = S.jc[i];
+            if (sel == SW_EV_SELECT) {
+                const int n = S.arr[SW_A_N][i];
+                fa = fa + sw_f(&c, n, S.nb, S.beta, S.ell);
+                fb = fb + sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell);
+                gm = sw_max(gm, sw_g(&c, n));
+            } else if (sel == SW_EV_GMAX) {
+                gm = sw_max(gm, sw_g(&c, S.arr[arg][i]));
+            } else if (sel == SW_EV_PACKED) {
+                const int pl = S.arr[arg][i];
+                fa = fa + sw_f(&c, pl, S.nb, S.beta, S.ell);
+                gm = sw_max(gm, sw_g(&c, pl));
+                is += (long long)c.w * (S.arr[SW_A_NB][i] - pl);
+            } else if (sel == SW_EV_P2OK) {
+                is += S.arr[SW_A_PL][i] != S.arr[SW_A_NFIN][i];
+            } else { /* SW_EV_FINAL */
+                const uint64_t m = S.y[arg][i];
+                const int cn = __popcll(m);
+                long long Ssum = 0;
+                for (int t = 0; t < S.T; ++t) {
+                    const uint32_t bit = (uint32_t)((m >> t) & 1ull);
+                    Ssum += bit ? t : 0;
+                    S.plan[(size_t)i * S.T + t] = (uint8_t)bit;
+                }
+                S.planned[i] = cn;
+                fa = fa + sw_f(&c, cn, S.nb, S.beta, S.ell);
+                fb = fb + (cn > 0 ? ((double)Ssum / (double)cn) * S.p[i] : 0.0);
+                gm = sw_max(gm, sw_g(&c, cn));
+                is += cn > 0;
+            }
+        }
+        out[lane] = fa;
+        out[S.LW + lane] = fb;
+    }
+    const uint64_t gw = wave_max(sw_bits(gm));
+    const long long iw = wave_sum(is);
+    if (lane_id() == 0) { sg[wave_id()] = gw; ss[wave_id()] = iw; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t g = 0;
+        long long s = 0;
+        for (int w = 0; w < SW_WAVES; ++w) { g = sg[w] > g ? sg[w] : g; s += ss[w]; }
+        out[2 * S.LW] = sw_from_bits(g);
+        reinterpret_cast<long long*>(out)[2 * S.LW + 1] = s;
+    }
+}
+
+/* ---- placement ---------------------------------------------------------------- */
+
+/* this rank's entries (twin: the k1/k2 of each pack caller) */
+__global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, int src, double Mb,
+                                                   sw_pack_ent* out) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.P) return;
+    sw_pack_ent e;
+    e.khi = 0; e.klo = 0; e.st = 0; e.pad = 0;
+    if (i < S.NL) {
+        const int n = S.arr[src][i];
+        if (n > 0) {
+            const sw_jobc c = S.jc[i];
+            uint64_t k1;
+            uint32_t k2;
+            if (mode != 2) {
+                const double lvl = sw_g(&c, n - 1);
+                const bool crit = S.k > 0.0 && lvl > Mb;
+                k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)c.w : 0);
+                k2 = sw_fbits_of(S.keys[(size_t)i * S.T + n - 1]);
+            } else {
+                k1 = sw_bits(S.p[i] / (double)n);
+                k2 = 0;
+            }
+            e.khi = k1;
+            e.klo = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(S.off + i));
+            e.st = (uint32_t)n | ((uint32_t)c.w << 8);
+        }
+    }
+    out[i] = e;
+}
+
+/* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') > key(e)} */
+constexpr int kRankTile = 1024;
+__global__ __launch_bounds__(kTB) void k_pack_rank(const sw_pack_ent* all, int64_t M, int32_t* rank) {
+    __shared__ uint64_t th[kRankTile], tl[kRankTile];
+    const int64_t t0 = (int64_t)blockIdx.y * kRankTile;
+    for (int x = threadIdx.x; x < kRankTile; x += kTB) {
+        const int64_t e = t0 + x;
+        const bool act = e < M && all[e].st != 0;
+        th[x] = act ? all[e].khi : 0;
+        tl[x] = act ? all[e].klo : 0; /* inactive: (0,0) never exceeds an active key */
+    }
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (e >= M || all[e].st == 0) return;
+    const uint64_t h = all[e].khi, l = all[e].klo;
+    int c = 0;
+    const int n = (int)min((int64_t)kRankTile, M - t0);
+    for (int x = 0; x < n; ++x) c += (th[x] > h) || (th[x] == h && tl[x] > l);
+    if (c) atomicAdd(&rank[e], c);
+}
+
+__global__ __launch_bounds__(kTB) void k_pack_scatter(const sw_pack_ent* all, int64_t M,
+                                                      const int32_t* rank, int32_t* order) {
+    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (e < M && all[e].st != 0) order[rank[e]] = (int32_t)e;
+}
+
+/* the round loop over the global order; writes this rank's rows */
+template <int E>
+__global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
+                                                          int64_t M, const int32_t* order,
+                                                          int ydst, int pdst) {
+    __shared__ sw_xchg X;
+    __shared__ sw_pack_lds PL;
+    sw_blk blk;
+    blk.X = &X;
+    blk.par = 0;
+    const int tid = threadIdx.x;
+    int act = 0;
+    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
+    const int A = blk.sum32(act);
+    for (int i = tid; i < S.NL; i += SW_BLOCK) { S.y[ydst][i] = 0; S.arr[pdst][i] = 0; }
+    uint32_t st[E];
+    uint64_t mk[E];
+    int32_t ent[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        const int p = E * tid + i;
+        ent[i] = p < A ? order[p] : -1;
+        st[i] = p < A ? all[ent[i]].st : 0u;
+    }
+    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk);
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        if (ent[i] < 0) continue;
+        const int64_t j = (int64_t)(0xFFFFFFFFu - (uint32_t)(all[ent[i]].klo & 0xFFFFFFFFu));
+        if (j >= S.off && j < S.off + S.NL) {
+            S.y[ydst][j - S.off] = mk[i];
+            S.arr[pdst][j - S.off] = (int32_t)(all[ent[i]].st & 0xFFu) - (int32_t)pk_r(st[i]);
+        }
+    }
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n + kTB - 1) / kTB : 1); }
+
+}  // namespace
+
+/* ---- host side: the engine behind sw_shard_ops ------------------------------ */
+
+struct sw_shard_state {
+    sw_handle* h = nullptr;
+    int32_t rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    bool host_comm = false;
+    sw_host_comm hc;
+    /* current solve */
+    int32_t NL = 0, T = 0;
+    int64_t N = 0, off = 0, q = 1, P = 0, LW = 0;
+    double delta = 0.0;
+    ShardDev dv;
+    /* device */
+    DevBuf<int32_t> w, F, E, l, taken, arr[SW_A_COUNT], planned, prank, porder;
+    DevBuf<double> d, R, p, xsend, xrecv;
+    DevBuf<sw_jobc> jc;
+    DevBuf<float> keys;
+    DevBuf<uint64_t> y[SW_Y_COUNT];
+    DevBuf<uint8_t> plan;
+    DevBuf<long long> red;
+    DevBuf<sw_pack_ent> psend, pall;
+    /* pinned staging */
+    HostBuf<uint8_t> hx;
+    std::vector<int32_t> w_all;
+    std::vector<uint8_t> hgather;
+};
+
+namespace {
+
+#define SH_HIP(S, call)                                                                    \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            (S)->h->err = std::string(#call) + ": " + hipGetErrorString(e_);               \
+            return SW_ERR_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+#define SH_NCCL(S, call)                                                                   \
+    do {                                                                                   \
+        ncclResult_t r_ = (call);                                                          \
+        if (r_ != ncclSuccess) {                                                           \
+            (S)->h->err = std::string(#call) + ": " + ncclGetErrorString(r_);              \
+            return SW_ERR_RCCL;                                                            \
+        }                                                                                  \
+    } while (0)
+
+#define SH_TRY(x)                \
+    do {                         \
+        int rc_ = (x);           \
+        if (rc_ < 0) return rc_; \
+    } while (0)
+
+int host_fail(sw_shard_state* S, const char* what) {
+    S->h->err = std::string("host collective failed: ") + what;
+    return SW_ERR_RCCL;
+}
+
+/* In-place all-reduce of n values on the device buffer `dbuf`, copied to
+ * `hout`.  op: 0 = sum i64, 1 = max u64, 2 = max f64. */
+int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
+    hipStream_t st = S->h->stream;
+    const size_t bytes = (size_t)n * 8;
+    if (S->comm) {
+        const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
+        SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
+    }
+    SH_HIP(S, hipMemcpyAsync(S->hx.p, dbuf, bytes, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipStreamSynchronize(st));
+    memcpy(hout, S->hx.p, bytes);
+    if (S->world > 1 && S->host_comm) {
+        int rc = op == 0 ? S->hc.allreduce_sum_i64(S->hc.ctx, (int64_t*)hout, n)
+               : op == 1 ? S->hc.allreduce_max_u64(S->hc.ctx, (uint64_t*)hout, n)
+                         : S->hc.allreduce_max_f64(S->hc.ctx, (double*)hout, n);
+        if (rc) return host_fail(S, "all-reduce");
+    }
+    return SW_OK;
+}
+
+/* All-gather `bytes` per rank from dsend into drecv (device, rank order).
+ * If hrecv is set, the gathered blocks are also copied to the host. */
+int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes, void* hrecv) {
+    hipStream_t st = S->h->stream;
+    const size_t total = bytes * (size_t)S->world;
+    if (!S->host_comm) {
+        if (!S->comm) {
+            if (drecv != dsend)
+                SH_HIP(S, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, st));
+        } else {
+            SH_NCCL(S, ncclAllGather(dsend, drecv, bytes, ncclUint8, S->comm, st));
+        }
+        if (hrecv) {
+            if (S->hx.reserve(total)) return host_fail(S, "pinned staging");
+            SH_HIP(S, hipMemcpyAsync(S->hx.p, drecv, total, hipMemcpyDeviceToHost, st));
+            SH_HIP(S, hipStreamSynchronize(st));
+            memcpy(hrecv, S->hx.p, total);
+        }
+        return SW_OK;
+    }
+    /* host collectives: down, gather, up */
+    if (S->hx.reserve(total)) return host_fail(S, "pinned staging");
+    S->hgather.resize(total);
+    SH_HIP(S, hipMemcpyAsync(S->hx.p, dsend, bytes, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipStreamSynchronize(st));
+    std::vector<uint8_t> mine(S->hx.p, S->hx.p + bytes);
+    if (S->hc.allgather(S->hc.ctx, mine.data(), S->hgather.data(), (int64_t)bytes))
+        return host_fail(S, "all-gather");
+    memcpy(S->hx.p, S->hgather.data(), total);
+    SH_HIP(S, hipMemcpyAsync(drecv, S->hx.p, total, hipMemcpyHostToDevice, st));
+    if (hrecv) memcpy(hrecv, S->hgather.data(), total);
+    SH_HIP(S, hipStreamSynchronize(st)); /* staging is reused by the next step */
+    return SW_OK;
+}
+
+int zero_red(sw_shard_state* S, int n) {
+    SH_HIP(S, hipMemsetAsync(S->red.p, 0, (size_t)n * 8, S->h->stream));
+    return SW_OK;
+}
+
+#define LAUNCH(S, ...)                                   \
+    do {                                                 \
+        hipLaunchKernelGGL(__VA_ARGS__);                 \
+        SH_HIP(S, hipGetLastError());                    \
+    } while (0)
+
+/* ---- sw_shard_ops ---------------------------------------------------------- */
+
+int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    SH_TRY(zero_red(S, 2));
+    LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->w.p, S->d.p, S->F.p,
+           S->E.p, S->R.p, S->delta);
+    uint64_t mx[2];
+    SH_TRY(coll_reduce(S, S->red.p, 2, 1, mx));
+    if (S->host_comm && S->world > 1) { /* kernels read A from red[0] */
+        memcpy(S->hx.p, mx, 16);
+        SH_HIP(S, hipMemcpyAsync(S->red.p, S->hx.p, 16, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipStreamSynchronize(st));
+    }
+    LAUNCH(S, k_keys, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv);
+    *A = sw_from_bits(mx[0]);
+    *lb = sw_from_bits(mx[1]);
+    /* every job's width, gathered once (the width tail needs w of the winner) */
+    int32_t* wsend = (int32_t*)S->xsend.p;
+    int32_t* wrecv = (int32_t*)S->xrecv.p;
+    SH_HIP(S, hipMemsetAsync(wsend, 0, (size_t)S->P * 4, st));
+    if (S->NL) SH_HIP(S, hipMemcpyAsync(wsend, S->w.p, (size_t)S->NL * 4, hipMemcpyDeviceToDevice, st));
+    S->w_all.resize((size_t)S->P * S->world);
+    SH_TRY(coll_gather(S, wsend, wrecv, (size_t)S->P * 4, S->w_all.data()));
+    for (int64_t j = 0; j < S->N; ++j) w_all[j] = S->w_all[j]; /* rank r's block starts at job r·P */
+    return SW_OK;
+}
+
+int op_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 2));
+    LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, M, (int)is_inf);
+    return coll_reduce(S, S->red.p, 2, 0, out);
+}
+
+template <bool LEVEL>
+int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
+    Thresholds th;
+    th.K = K;
+    for (int i = 0; i < K; ++i) th.v[i] = v[i];
+    SH_TRY(zero_red(S, K + 1));
+    LAUNCH(S, k_probe<LEVEL>, dim3(nblk((int64_t)S->NL * S->T)), dim3(kTB), 0, S->h->stream, S->dv, th);
+    int64_t bins[SW_SHARD_K + 1];
+    SH_TRY(coll_reduce(S, S->red.p, K + 1, 0, bins));
+    int64_t suf = 0;
+    for (int i = K - 1; i >= 0; --i) { suf += bins[i + 1]; out[i] = suf; }
+    return SW_OK;
+}
+
+int op_count_gt(void* ctx, const uint32_t* rho, int32_t K, int64_t* out) {
+    uint64_t v[SW_SHARD_K];
+    for (int i = 0; i < K; ++i) v[i] = rho[i];
+    return probe<false>((sw_shard_state*)ctx, v, K, out);
+}
+
+int op_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
+    uint64_t v[SW_SHARD_K];
+    for (int i = 0; i < K; ++i) v[i] = sw_bits(M[i]);
+    return probe<true>((sw_shard_state*)ctx, v, K, out);
+}
+
+int op_between(void* ctx, double a, double b, int64_t* out) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 1));
+    LAUNCH(S, k_between, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, a, b);
+    return coll_reduce(S, S->red.p, 1, 0, out);
+}
+
+int op_take_all(void* ctx) {
+    auto* S = (sw_shard_state*)ctx;
+    LAUNCH(S, k_take_all, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv);
+    return SW_OK;
+}
+
+int op_take(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 2));
+    LAUNCH(S, k_take, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, rho);
+    std::vector<int64_t> all((size_t)2 * S->world);
+    SH_TRY(coll_gather(S, S->red.p, S->xrecv.p, 16, all.data()));
+    *wt = 0;
+    *excl = 0;
+    for (int r = 0; r < S->world; ++r) {
+        *wt += all[2 * r];
+        if (r < S->rank) *excl += all[2 * r + 1];
+    }
+    return SW_OK;
+}
+
+int op_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 1));
+    LAUNCH(S, k_assign, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, rho, (long long)rem,
+           (long long)excl);
+    return coll_reduce(S, S->red.p, 1, 0, used);
+}
+
+int op_tail_best(void* ctx, int64_t rem2, uint64_t* best) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 1));
+    LAUNCH(S, k_tail_best, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (long long)rem2);
+    return coll_reduce(S, S->red.p, 1, 1, best);
+}
+
+int op_tail_apply(void* ctx, int64_t jb) {
+    auto* S = (sw_shard_state*)ctx;
+    if (jb >= S->off && jb < S->off + S->NL)
+        LAUNCH(S, k_tail_apply, dim3(1), dim3(1), 0, S->h->stream, S->dv, (int)(jb - S->off));
+    return SW_OK;
+}
+
+int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
+            int64_t* isum) {
+    auto* S = (sw_shard_state*)ctx;
+    const int64_t LW = S->LW, blk = 2 * LW + 2;
+    LAUNCH(S, k_eval, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, (int)sel, (int)arg, S->xsend.p);
+    std::vector<double> all((size_t)blk * S->world);
+    SH_TRY(coll_gather(S, S->xsend.p, S->xrecv.p, (size_t)blk * 8, all.data()));
+    double g = 0.0;
+    int64_t s = 0;
+    for (int r = 0; r < S->world; ++r) {
+        const double* b = all.data() + (size_t)r * blk;
+        memcpy(lanesA + r * LW, b, (size_t)LW * 8);
+        memcpy(lanesB + r * LW, b + LW, (size_t)LW * 8);
+        g = sw_max(g, b[2 * LW]);
+        int64_t v;
+        memcpy(&v, b + 2 * LW + 1, 8);
+        s += v;
+    }
+    *gm = g;
+    *isum = s;
+    return SW_OK;
+}
+
+int op_copy(void* ctx, int32_t dst, int32_t src) {
+    auto* S = (sw_shard_state*)ctx;
+    if (S->NL)
+        SH_HIP(S, hipMemcpyAsync(S->arr[dst].p, S->arr[src].p, (size_t)S->NL * 4,
+                                 hipMemcpyDeviceToDevice, S->h->stream));
+    return SW_OK;
+}
+
+int op_copy_y(void* ctx, int32_t dst, int32_t src) {
+    auto* S = (sw_shard_state*)ctx;
+    if (S->NL)
+        SH_HIP(S, hipMemcpyAsync(S->y[dst].p, S->y[src].p, (size_t)S->NL * 8,
+                                 hipMemcpyDeviceToDevice, S->h->stream));
+    return SW_OK;
+}
+
+int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    const int64_t M = S->P * S->world;
+    LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, (int)src, Mb, S->psend.p);
+    SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr));
+    SH_HIP(S, hipMemsetAsync(S->prank.p, 0, (size_t)M * 4, st));
+    dim3 g2(nblk(M), (unsigned)((M + kRankTile - 1) / kRankTile));
+    LAUNCH(S, k_pack_rank, g2, dim3(kTB), 0, st, S->pall.p, M, S->prank.p);
+    LAUNCH(S, k_pack_scatter, dim3(nblk(M)), dim3(kTB), 0, st, S->pall.p, M, S->prank.p, S->porder.p);
+    const ShardDev dv = S->dv;
+    if (M <= 2 * SW_BLOCK)
+        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+    else if (M <= 8 * SW_BLOCK)
+        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+    else if (M <= 32 * SW_BLOCK)
+        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+    else if (M <= 64 * SW_BLOCK)
+        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+    else
+        return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
+    return SW_OK;
+}
+
+/* Reserve the per-solve buffers and upload this rank's jobs. */
+int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
+    hipStream_t st = S->h->stream;
+    S->NL = pr->num_jobs;
+    S->T = pr->future_rounds;
+    S->N = N;
+    S->off = off;
+    S->q = (N + SW_DET_LANES - 1) / SW_DET_LANES;
+    if (S->q == 0) S->q = 1;
+    S->LW = SW_DET_LANES / S->world;
+    S->P = S->LW * S->q;
+    S->delta = pr->round_duration;
+    const size_t NL = (size_t)std::max<int32_t>(S->NL, 1), T = (size_t)S->T;
+    const size_t M = (size_t)S->P * S->world;
+    const size_t xbytes = std::max<size_t>({(size_t)(2 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
+    bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
+               S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
+               S->l.reserve(NL) || S->taken.reserve(NL) || S->plan.reserve(NL * T) ||
+               S->planned.reserve(NL) || S->red.reserve(kRed) ||
+               S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
+               S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
+               S->porder.reserve(M);
+    for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
+    for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
+    if (bad || S->hx.reserve(std::max<size_t>(xbytes * S->world, kRed * 8)))
+        return S->h->err = "shard allocation failed", SW_ERR_HIP;
+    if (S->NL) {
+        const size_t n = (size_t)S->NL;
+        SH_HIP(S, hipMemcpyAsync(S->w.p, pr->nworkers, n * 4, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->F.p, pr->completed_epochs, n * 4, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->E.p, pr->total_epochs, n * 4, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->d.p, pr->epoch_duration, n * 8, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->R.p, pr->remaining_runtime, n * 8, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->p.p, pr->priority, n * 8, hipMemcpyHostToDevice, st));
+        for (int a = 0; a < SW_A_COUNT; ++a)
+            SH_HIP(S, hipMemsetAsync(S->arr[a].p, 0, n * 4, st));
+        for (int a = 0; a < SW_Y_COUNT; ++a)
+            SH_HIP(S, hipMemsetAsync(S->y[a].p, 0, n * 8, st));
+        SH_HIP(S, hipMemsetAsync(S->l.p, 0, n * 4, st));
+        SH_HIP(S, hipMemsetAsync(S->taken.p, 0, n * 4, st));
+    }
+    ShardDev& v = S->dv;
+    memset(&v, 0, sizeof(v));
+    v.NL = S->NL; v.T = S->T; v.G = pr->num_gpus; v.nb = pr->num_bases;
+    v.LW = (int32_t)S->LW; v.rank = S->rank;
+    v.off = off; v.N = N; v.q = S->q; v.P = S->P;
+    v.k = pr->regularizer;
+    for (int b = 0; b < SW_BMAX; ++b) {
+        v.beta[b] = b < pr->num_bases ? pr->bases[b] : 0.0;
+        v.ell[b] = b < pr->num_bases ? pr->log_bases[b] : 0.0;
+    }
+    v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->p.p; v.l = S->l.p; v.taken = S->taken.p;
+    for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
+    for (int a = 0; a < SW_Y_COUNT; ++a) v.y[a] = S->y[a].p;
+    v.plan = S->plan.p; v.planned = S->planned.p; v.red = S->red.p;
+    return SW_OK;
+}
+
+int shard_attach(sw_handle* h, int32_t rank, int32_t world) {
+    if (!h) return SW_ERR_INVALID;
+    int64_t lo, hi;
+    if (sw_shard_range(0, world, rank, &lo, &hi) != 0)
+        return h->err = "world must divide 512 and 0 <= rank < world", SW_ERR_INVALID;
+    sw_shard_release(h);
+    h->shard = new (std::nothrow) sw_shard_state();
+    if (!h->shard) return h->err = "out of host memory", SW_ERR_HIP;
+    h->shard->h = h;
+    h->shard->rank = rank;
+    h->shard->world = world;
+    return SW_OK;
+}
+
+}  // namespace
+
+void sw_shard_release(sw_handle* h) {
+    if (!h || !h->shard) return;
+    sw_shard_state* S = h->shard;
+    if (S->comm) (void)ncclCommDestroy(S->comm);
+    S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
+    S->planned.release(); S->prank.release(); S->porder.release(); S->d.release(); S->R.release();
+    S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
+    S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
+    for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
+    for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
+    delete S;
+    h->shard = nullptr;
+}
+
+extern "C" {
+
+int sw_dist_shard_range(int64_t total_jobs, int32_t world, int32_t rank, int64_t* lo, int64_t* hi) {
+    if (!lo || !hi) return SW_ERR_INVALID;
+    return sw_shard_range(total_jobs, world, rank, lo, hi) == 0 ? SW_OK : SW_ERR_INVALID;
+}
+
+int sw_dist_unique_id(void* out_bytes) {
+    if (!out_bytes) return SW_ERR_INVALID;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SW_ERR_RCCL;
+    memcpy(out_bytes, id.internal, SW_NCCL_UNIQUE_ID_BYTES);
+    return SW_OK;
+}
+
+int sw_dist_init(sw_handle* h, const void* unique_id, int32_t rank, int32_t world) {
+    if (!h || !unique_id) return SW_ERR_INVALID;
+    SH_TRY(shard_attach(h, rank, world));
+    {
+        /* world 1 too: the collectives then run through RCCL as at world > 1 */
+        ncclUniqueId id;
+        memcpy(id.internal, unique_id, SW_NCCL_UNIQUE_ID_BYTES);
+        if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
+        ncclResult_t r = ncclCommInitRank(&h->shard->comm, world, id, rank);
+        if (r != ncclSuccess) {
+            h->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            h->shard->comm = nullptr;
+            sw_shard_release(h);
+            return SW_ERR_RCCL;
+        }
+    }
+    return SW_OK;
+}
+
+int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int32_t world) {
+    if (!h || !comm || !comm->allreduce_sum_i64 || !comm->allreduce_max_u64 ||
+        !comm->allreduce_max_f64 || !comm->allgather)
+        return SW_ERR_INVALID;
+    SH_TRY(shard_attach(h, rank, world));
+    h->shard->host_comm = true;
+    h->shard->hc = *comm;
+    return SW_OK;
+}
+
+int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
+                       sw_result* res) {
+    if (!h || !res) return SW_ERR_INVALID;
+    if (!h->shard) return h->err = "sw_dist_init / sw_dist_init_host first", SW_ERR_INVALID;
+    sw_shard_state* S = h->shard;
+    if (sw_validate_problem(local) != 0) return h->err = "invalid problem", SW_ERR_INVALID;
+    int64_t lo, hi;
+    if (sw_shard_range(total_jobs, S->world, S->rank, &lo, &hi) != 0 || lo != job_offset ||
+        hi - lo != local->num_jobs)
+        return h->err = "slice does not match sw_dist_shard_range", SW_ERR_INVALID;
+    if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
+    SH_TRY(prepare(S, local, job_offset, total_jobs));
+    sw_shard_ops ops;
+    ops.ctx = S;
+    ops.setup = op_setup;
+    ops.force = op_force;
+    ops.count_gt = op_count_gt;
+    ops.feasible = op_feasible;
+    ops.between = op_between;
+    ops.take_all = op_take_all;
+    ops.take = op_take;
+    ops.assign = op_assign;
+    ops.tail_best = op_tail_best;
+    ops.tail_apply = op_tail_apply;
+    ops.eval = op_eval;
+    ops.copy = op_copy;
+    ops.copy_y = op_copy_y;
+    ops.pack = op_pack;
+    int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
+                            local->regularizer, &res->objective, &res->utility, &res->makespan,
+                            &res->p2_objective, &res->bound, &res->iters, &res->status);
+    if (rc < 0) return rc == -1 ? (h->err = "out of host memory", SW_ERR_HIP) : rc;
+    const size_t n = (size_t)S->NL;
+    if (n) {
+        if (res->plan)
+            SH_HIP(S, hipMemcpyAsync(res->plan, S->plan.p, n * S->T, hipMemcpyDeviceToHost, h->stream));
+        if (res->planned_rounds)
+            SH_HIP(S, hipMemcpyAsync(res->planned_rounds, S->planned.p, n * 4, hipMemcpyDeviceToHost,
+                                     h->stream));
+    }
+    SH_HIP(S, hipStreamSynchronize(h->stream));
+    return rc;
+}
+
+}  // extern "C"

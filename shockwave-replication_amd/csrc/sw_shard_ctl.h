@@ -1,0 +1,388 @@
+/*
+ * sw_shard_ctl.h — controller of the SHARDED single-instance plan solve
+ * (jobs split across ranks, one process per GPU).
+ *
+ * Plain C99 (compiled by hipcc into the product library and by gcc into the
+ * CPU test engine oracle/shard_twin.c).  The controller is the algorithm of
+ * oracle/plan_twin.c rewritten as a sequence of STEPS; every
+ * step is a local pass over this rank's jobs followed by one collective, done
+ * by a "shard engine" behind the sw_shard_ops table:
+ *
+ *   product engine  sw_shard.hip   — HIP kernels over the rank's jobs in HBM,
+ *                                    RCCL (xGMI) or host collectives
+ *   CPU engine      oracle/shard_twin.c — test infrastructure only
+ *
+ * Every engine returns GLOBAL values (after its collective), so the control
+ * flow is identical on every rank.
+ *
+ * Bit-identity with the single-instance solve.  Jobs are sharded along the
+ * SW_DET_LANES lanes of the deterministic sum (sw_detsum: lane L sums jobs
+ * [L·q, (L+1)·q), q = ⌈N/512⌉): rank r owns lanes [r·512/W, (r+1)·512/W) and
+ * therefore jobs [r·(512/W)·q, (r+1)·(512/W)·q) (sw_shard_range).  Engines
+ * return the per-lane partial sums of their own lanes, gathered in rank
+ * order, and the controller runs the same halving tree as sw_detsum.  Integer
+ * sums and maxima are order free, the tie group's job-ordered prefix becomes
+ * a rank-exclusive prefix, and the width tail's arg-max is a global max of
+ * (key, ~job).  So for every world size W | 512 the sharded solve returns the
+ * same plan, counts and objective bits as sw_plan_solve / plan_twin.c on the
+ * whole instance (tests/test_shard.py).
+ *
+ * Fewer collectives.  The two bisections of the twin (the fp32 price bits in
+ * SELECT, the fp64 makespan bits of the feasibility search) become K-ary
+ * searches: one step evaluates up to SW_SHARD_K thresholds and one
+ * all-reduce carries all K counts.  The predicate is monotone, so the K-ary
+ * search returns exactly the bisection's answer in ⌈bits / log2(K+1)⌉ steps
+ * (31 → 6 for the price, ≤ 64 → 11 for the level).
+ */
+#ifndef SW_SHARD_CTL_H
+#define SW_SHARD_CTL_H
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "sw_arith.h"
+
+#define SW_SHARD_K 63 /* thresholds evaluated per search step (≤ 63) */
+
+/* per-job count arrays an engine keeps for its jobs */
+enum {
+    SW_A_N = 0,     /* current SELECT counts (twin: n)             */
+    SW_A_NB = 1,    /* best level-search counts (twin: nb)         */
+    SW_A_NFIN = 2,  /* best packed P1 counts (twin: nbest)         */
+    SW_A_PL = 3,    /* placed counts of the last pack (twin: placed) */
+    SW_A_PL2 = 4,   /* placed counts of pack order B (placed2)     */
+    SW_A_COUNT = 5
+};
+/* per-job round bitmasks (bit t = runs in future round t) */
+enum { SW_Y_CUR = 0, SW_Y_BEST = 1, SW_Y_2 = 2, SW_Y_COUNT = 3 };
+
+/* eval selectors: which per-job quantities a reduction step sums */
+enum {
+    SW_EV_SELECT = 0, /* A: f(n)  B: f(l + taken)  gm: g(n)                        */
+    SW_EV_GMAX = 1,   /* gm: g(arr[arg])                                             */
+    SW_EV_PACKED = 2, /* A: f(arr[arg])  gm: g(arr[arg])  isum: Σ w·(nb − arr[arg])  */
+    SW_EV_P2OK = 3,   /* isum: #{j : placed ≠ nfin}                                  */
+    SW_EV_FINAL = 4   /* y = Y[arg]: c = popcount(y); A: f(c)  B: S(y)/c·p  gm: g(c)
+                         isum: #{c > 0}; also writes the plan rows and counts        */
+};
+
+typedef struct sw_shard_ops {
+    void* ctx;
+    /* constants, key rows; A = max_j a_j, lb = max_j g_j(T_j); w_all[N] = every
+     * job's width (gathered) */
+    int (*setup)(void* ctx, double* A, double* lb, int32_t* w_all);
+    /* l_j := #{n < T_j : g_j(n) > M} (0 if is_inf); out = (Σ w·l, Σ w·(T_j − l)) */
+    int (*force)(void* ctx, double M, int32_t is_inf, int64_t out[2]);
+    /* out[i] = Σ w·#{n ∈ [l_j, T_j) : key_j(n) > rho[i]} */
+    int (*count_gt)(void* ctx, const uint32_t* rho, int32_t K, int64_t* out);
+    /* out[i] = Σ w·#{n < T_j : g_j(n) > M[i]} */
+    int (*feasible)(void* ctx, const double* M, int32_t K, int64_t* out);
+    /* out = #{(j, n ≤ T_j) : a < g_j(n) < b} */
+    int (*between)(void* ctx, double a, double b, int64_t* out);
+    /* n := T_j, taken := T_j − l */
+    int (*take_all)(void* ctx);
+    /* taken_j := count(key > rho), tie_j := count(key ≥ rho) − taken_j;
+     * wt = Σ_all w·taken, excl = Σ over ranks before this one of w·tie */
+    int (*take)(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl);
+    /* tie group in job order; n := l + taken + tt; used = Σ_all w·tt */
+    int (*assign)(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used);
+    /* max over jobs with n < T_j and w ≤ rem2 of key(n) << 32 | ~j (0 if none) */
+    int (*tail_best)(void* ctx, int64_t rem2, uint64_t* best);
+    /* n[jb] += 1 on the rank owning global job jb */
+    int (*tail_apply)(void* ctx, int64_t jb);
+    /* reductions: lanesA/lanesB receive all SW_DET_LANES lane partials (rank
+     * order), gm the max, isum the integer sum */
+    int (*eval)(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
+                int64_t* isum);
+    int (*copy)(void* ctx, int32_t dst, int32_t src);   /* count arrays */
+    int (*copy_y)(void* ctx, int32_t dst, int32_t src); /* bitmask arrays */
+    /* place arr[src] rounds per job (twin: pack); mode 1/3 = P1 orders A/B
+     * (Mb = makespan of arr[src]), 2 = P2 order p/n.  Writes Y[ydst], arr[pdst] */
+    int (*pack)(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst);
+} sw_shard_ops;
+
+/* Job range of `rank` (sw_dist_shard_range in include/shockwave_amd.h). */
+static inline int sw_shard_range(int64_t N, int32_t world, int32_t rank, int64_t* lo, int64_t* hi) {
+    if (world < 1 || world > SW_DET_LANES || (SW_DET_LANES % world) != 0 || rank < 0 ||
+        rank >= world || N < 0)
+        return -1;
+    const int64_t q = (N + SW_DET_LANES - 1) / SW_DET_LANES;
+    const int64_t per = (int64_t)(SW_DET_LANES / world) * q;
+    int64_t a = (int64_t)rank * per, b = a + per;
+    *lo = a < N ? a : N;
+    *hi = b < N ? b : N;
+    return 0;
+}
+
+/* The combining phase of sw_detsum (oracle/plan_twin.c) over the lane partials. */
+static inline double sw_shard_tree(const double* lanes) {
+    double part[SW_DET_LANES];
+    double wsum[SW_DET_LANES / 64];
+    memcpy(part, lanes, sizeof(part));
+    for (int32_t w = 0; w < SW_DET_LANES / 64; ++w) {
+        double* p = part + 64 * w;
+        for (int32_t h = 32; h >= 1; h >>= 1)
+            for (int32_t i = 0; i < h; ++i) p[i] = p[i] + p[i + h];
+        wsum[w] = p[0];
+    }
+    for (int32_t h = SW_DET_LANES / 128; h >= 1; h >>= 1)
+        for (int32_t i = 0; i < h; ++i) wsum[i] = wsum[i] + wsum[i + h];
+    return wsum[0];
+}
+
+typedef struct {
+    const sw_shard_ops* ops;
+    int64_t N;
+    int32_t T, G;
+    int64_t C;
+    double k, A, lb;
+    int32_t* w_all;
+    int64_t steps; /* collective steps taken (reported as iters) */
+    double lanesA[SW_DET_LANES], lanesB[SW_DET_LANES];
+} sw_shard_ctl;
+
+typedef struct {
+    double U, Mact, J, ubound;
+} sw_shard_eval;
+
+#define SWC_TRY(x)              \
+    do {                        \
+        int rc_ = (x);          \
+        if (rc_ < 0) return rc_; \
+    } while (0)
+
+/*
+ * K-ary search for the smallest x in [lo, hi) with pred(x) true, else hi —
+ * the twin's bisection `while (lo < hi) { mid; pred(mid) ? hi = mid : lo =
+ * mid + 1; }` for a monotone predicate.  kind 0: pred(x) = Σ w·cnt_gt(x) ≤
+ * bud (price bits); kind 1: pred(x) = Σ w·lforce(bits→double x) ≤ bud.
+ */
+static inline int swc_search(sw_shard_ctl* c, int kind, uint64_t lo, uint64_t hi, int64_t bud,
+                             uint64_t* out) {
+    uint64_t pts[SW_SHARD_K];
+    uint32_t rho[SW_SHARD_K];
+    double Ms[SW_SHARD_K];
+    int64_t cnt[SW_SHARD_K];
+    while (lo < hi) {
+        const uint64_t span = hi - lo;
+        const int32_t K = span < (uint64_t)SW_SHARD_K ? (int32_t)span : SW_SHARD_K;
+        const uint64_t d = (uint64_t)K + 1u, a = span / d, b = span % d;
+        for (int32_t i = 0; i < K; ++i) {
+            const uint64_t m = (uint64_t)(i + 1);
+            pts[i] = lo + a * m + (b * m) / d;
+            rho[i] = (uint32_t)pts[i];
+            Ms[i] = sw_from_bits(pts[i]);
+        }
+        if (kind == 0) SWC_TRY(c->ops->count_gt(c->ops->ctx, rho, K, cnt));
+        else SWC_TRY(c->ops->feasible(c->ops->ctx, Ms, K, cnt));
+        c->steps++;
+        int32_t f = K;
+        for (int32_t i = 0; i < K; ++i)
+            if (cnt[i] <= bud) { f = i; break; }
+        if (f < K) {
+            hi = pts[f];
+            if (f > 0) lo = pts[f - 1] + 1u;
+        } else {
+            lo = pts[K - 1] + 1u;
+        }
+    }
+    *out = lo;
+    return 0;
+}
+
+/* twin: select_level */
+static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eval* ev) {
+    const sw_shard_ops* o = c->ops;
+    int64_t wfa[2];
+    SWC_TRY(o->force(o->ctx, M, is_inf, wfa));
+    c->steps++;
+    const int64_t Wf = wfa[0], Wall = wfa[1];
+    if (Wf > c->C) {
+        ev->U = 0.0; ev->Mact = 0.0; ev->J = -1e308; ev->ubound = 0.0;
+        return 0;
+    }
+    const int64_t bud = c->C - Wf;
+    double rho_d = 0.0;
+    int64_t wgt_star;
+    if (Wall <= bud) {
+        SWC_TRY(o->take_all(o->ctx));
+        wgt_star = Wall;
+    } else {
+        uint64_t r64;
+        SWC_TRY(swc_search(c, 0, 0, SW_KEY_INF_BITS, bud, &r64));
+        const uint32_t rho = (uint32_t)r64;
+        rho_d = (double)sw_float_of(rho);
+        int64_t wt, excl, used;
+        SWC_TRY(o->take(o->ctx, rho, &wt, &excl));
+        c->steps++;
+        wgt_star = wt;
+        const int64_t rem = bud - wt;
+        SWC_TRY(o->assign(o->ctx, rho, rem, excl, &used));
+        c->steps++;
+        int64_t rem2 = rem - used;
+        while (rem2 > 0) {
+            uint64_t best;
+            SWC_TRY(o->tail_best(o->ctx, rem2, &best));
+            c->steps++;
+            if (best == 0) break;
+            const int64_t jb = (int64_t)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu));
+            SWC_TRY(o->tail_apply(o->ctx, jb));
+            rem2 -= c->w_all[jb];
+        }
+    }
+    double gm;
+    int64_t isum;
+    SWC_TRY(o->eval(o->ctx, SW_EV_SELECT, 0, c->lanesA, c->lanesB, &gm, &isum));
+    c->steps++;
+    ev->U = sw_shard_tree(c->lanesA);
+    ev->Mact = gm;
+    ev->J = ev->U - c->k * gm;
+    ev->ubound = sw_shard_tree(c->lanesB) + (rho_d * c->A) * (double)(bud - wgt_star);
+    return 0;
+}
+
+static inline int swc_keep(sw_shard_ctl* c, const sw_shard_eval* e, sw_shard_eval* best) {
+    if (e->J > best->J || (e->J == best->J && e->Mact < best->Mact)) {
+        *best = *e;
+        SWC_TRY(c->ops->copy(c->ops->ctx, SW_A_NB, SW_A_N));
+    }
+    return 0;
+}
+
+/* twin: level_search — best counts in SW_A_NB; *bound = U∞bound − k·M_lo */
+static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
+    const sw_shard_ops* o = c->ops;
+    sw_shard_eval ev, best;
+    SWC_TRY(swc_select(c, 0.0, 1, &ev));
+    best = ev;
+    const double U_inf = ev.U, M_free = ev.Mact, ub_inf = ev.ubound;
+    SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
+    double M_lo = M_free;
+    if (c->N > 0 && c->k > 0.0) {
+        uint64_t lo;
+        SWC_TRY(swc_search(c, 1, sw_bits(c->lb), sw_bits(M_free), c->C, &lo));
+        M_lo = sw_from_bits(lo);
+        SWC_TRY(swc_select(c, M_lo, 0, &ev));
+        SWC_TRY(swc_keep(c, &ev, &best));
+        const double width = (U_inf - ev.U) / c->k;
+        double a = M_lo, b = sw_min(M_free, M_lo + width);
+        for (int it = 0; it < SW_GS_ITERS; ++it) {
+            if (!(a < b)) break;
+            int64_t nbw;
+            SWC_TRY(o->between(o->ctx, a, b, &nbw));
+            c->steps++;
+            if (nbw == 0) break;
+            const double m1 = a + (b - a) * SW_GS_A;
+            const double m2 = a + (b - a) * SW_GS_B;
+            sw_shard_eval e1, e2;
+            SWC_TRY(swc_select(c, m1, 0, &e1));
+            SWC_TRY(swc_keep(c, &e1, &best));
+            SWC_TRY(swc_select(c, m2, 0, &e2));
+            SWC_TRY(swc_keep(c, &e2, &best));
+            if (e1.J >= e2.J) b = m2; else a = m1;
+        }
+    }
+    *bound = ub_inf - c->k * M_lo;
+    return 0;
+}
+
+/*
+ * The whole sharded plan solve (twin: twin_plan_solve).  Scalar results are
+ * global; the engine's SW_EV_FINAL step wrote this rank's plan rows.
+ * Returns SW_OK / SW_FALLBACK (1) or a negative engine error.
+ */
+static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, int32_t G, double k,
+                                 double* objective, double* utility, double* makespan,
+                                 double* p2_objective, double* bound_out, int32_t* iters,
+                                 int32_t* status_out) {
+    sw_shard_ctl* c = (sw_shard_ctl*)malloc(sizeof(sw_shard_ctl));
+    if (!c) return -1;
+    c->ops = o;
+    c->N = N;
+    c->T = T;
+    c->G = G;
+    c->C = (int64_t)G * T;
+    c->k = k;
+    c->steps = 0;
+    c->w_all = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    int rc = 0;
+    if (!c->w_all) { free(c); return -1; }
+#define SWC_RUN(x)                   \
+    do {                             \
+        rc = (x);                    \
+        if (rc < 0) goto done;       \
+    } while (0)
+    {
+        SWC_RUN(o->setup(o->ctx, &c->A, &c->lb, c->w_all));
+        c->steps++;
+        int32_t status = 0;
+        double bound = 0.0, Jbest = 0.0, gm;
+        int64_t isum;
+        for (int it = 0; it < SW_REPACK_ITERS; ++it) {
+            double b0;
+            SWC_RUN(swc_level_search(c, &b0));
+            if (it == 0) bound = b0;
+            double Mb;
+            SWC_RUN(o->eval(o->ctx, SW_EV_GMAX, SW_A_NB, c->lanesA, c->lanesB, &Mb, &isum));
+            c->steps++;
+            int64_t deficit = 0;
+            double Jp = 0.0;
+            for (int ord = 0; ord < 2; ++ord) {
+                const int32_t pdst = ord ? SW_A_PL2 : SW_A_PL;
+                SWC_RUN(o->pack(o->ctx, ord ? 3 : 1, SW_A_NB, Mb, ord ? SW_Y_2 : SW_Y_CUR, pdst));
+                c->steps++;
+                int64_t dfc;
+                SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, pdst, c->lanesA, c->lanesB, &gm, &dfc));
+                c->steps++;
+                const double Jo = sw_shard_tree(c->lanesA) - c->k * gm;
+                if (ord == 0 || Jo > Jp) {
+                    Jp = Jo;
+                    deficit = dfc;
+                    if (ord == 1) {
+                        SWC_RUN(o->copy(o->ctx, SW_A_PL, SW_A_PL2));
+                        SWC_RUN(o->copy_y(o->ctx, SW_Y_CUR, SW_Y_2));
+                    }
+                }
+                if (ord == 0 && dfc == 0) break;
+            }
+            if (it == 0 || Jp > Jbest) {
+                Jbest = Jp;
+                SWC_RUN(o->copy(o->ctx, SW_A_NFIN, SW_A_PL));
+                SWC_RUN(o->copy_y(o->ctx, SW_Y_BEST, SW_Y_CUR));
+            }
+            if (deficit == 0) break;
+            status |= SW_STATUS_P1_REPACKED;
+            c->C -= deficit;
+        }
+        /* P2: priority placement of the best packed counts (shockwave.py:281-328) */
+        SWC_RUN(o->pack(o->ctx, 2, SW_A_NFIN, 0.0, SW_Y_2, SW_A_PL));
+        c->steps++;
+        int64_t bad;
+        SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
+        c->steps++;
+        const int ok2 = bad == 0;
+        if (!ok2) status |= SW_STATUS_P2_FALLBACK;
+        int64_t any;
+        SWC_RUN(o->eval(o->ctx, SW_EV_FINAL, ok2 ? SW_Y_2 : SW_Y_BEST, c->lanesA, c->lanesB, &gm,
+                        &any));
+        c->steps++;
+        if (any == 0) status |= SW_STATUS_NO_PLANNED;
+        const double U = sw_shard_tree(c->lanesA);
+        *p2_objective = sw_shard_tree(c->lanesB);
+        *utility = U;
+        *makespan = gm;
+        *objective = U - k * gm;
+        *bound_out = bound;
+        *iters = (int32_t)c->steps;
+        *status_out = status;
+        rc = (status & SW_STATUS_P2_FALLBACK) ? SW_FALLBACK : SW_OK;
+    }
+done:
+#undef SWC_RUN
+    free(c->w_all);
+    free(c);
+    return rc;
+}
+
+#endif /* SW_SHARD_CTL_H */

@@ -7,7 +7,11 @@
  *     (the SOS2 interpolation of shockwave.py:162-179 needs an ordered grid);
  *   - Δ ≤ 0, k < 0 (k < 0 makes the reference's max-makespan term unbounded);
  *   - w < 1, E < 1, F ∉ [0, E] (job_metadata.py:75-78 asserts F ≤ E),
- *     d ≤ 0, non-finite R or priority < 0 (FTF^λ ≥ 0, shockwave.py:368).
+ *     d ≤ 0, non-finite R or priority < 0 (FTF^λ ≥ 0, shockwave.py:368);
+ *   - a schedulable job (w ≤ G) wider than SW_MAX_WIDTH GPUs: the placement
+ *     packs w into 8 bits (reference traces use scale factors 1–8).  Jobs
+ *     wider than the cluster are accepted at any width; they are never
+ *     scheduled (shockwave.py:64-75).
  */
 #ifndef SW_VALIDATE_H
 #define SW_VALIDATE_H
@@ -32,6 +36,7 @@ static inline int sw_validate_problem(const sw_problem* pr) {
         return -1;
     for (int32_t j = 0; j < pr->num_jobs; ++j) {
         if (pr->nworkers[j] < 1 || pr->total_epochs[j] < 1) return -1;
+        if (pr->nworkers[j] <= pr->num_gpus && pr->nworkers[j] > SW_MAX_WIDTH) return -1;
         if (pr->completed_epochs[j] < 0 || pr->completed_epochs[j] > pr->total_epochs[j]) return -1;
         if (!(pr->epoch_duration[j] > 0.0) || !sw_finite(pr->epoch_duration[j])) return -1;
         if (!sw_finite(pr->remaining_runtime[j])) return -1;

@@ -82,6 +82,102 @@ class SwConfig(C.Structure):
     ]
 
 
+# sw_host_comm (include/shockwave_amd.h): blocking host collectives
+ALLRED_I64 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_int32)
+ALLRED_U64 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int32)
+ALLRED_F64 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32)
+ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
+
+class SwHostComm(C.Structure):
+    _fields_ = [
+        ("ctx", C.c_void_p),
+        ("allreduce_sum_i64", ALLRED_I64),
+        ("allreduce_max_u64", ALLRED_U64),
+        ("allreduce_max_f64", ALLRED_F64),
+        ("allgather", ALLGATHER),
+    ]
+
+
+class HostComm:
+    """sw_host_comm backed by Python collectives.
+
+    ``impl`` provides ``allgather_bytes(bytes) -> list[bytes]`` (rank order);
+    every reduction is built from it, so any transport works: a
+    torch.distributed gloo group (TorchGroupComm), or threads in tests.  The
+    ctypes callbacks are kept alive by this object.
+    """
+
+    def __init__(self, impl):
+        self.impl = impl
+        self.error = None
+
+        def guard(fn):
+            def run(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except Exception as e:  # reported through the solve's return code
+                    self.error = e
+                    return -1
+            return run
+
+        def sum_i64(_ctx, buf, n):
+            v = np.ctypeslib.as_array(buf, (n,))
+            parts = self.impl.allgather_bytes(v.tobytes())
+            v[:] = np.sum([np.frombuffer(b, np.int64) for b in parts], axis=0)
+
+        def max_u64(_ctx, buf, n):
+            v = np.ctypeslib.as_array(buf, (n,))
+            parts = self.impl.allgather_bytes(v.tobytes())
+            v[:] = np.max([np.frombuffer(b, np.uint64) for b in parts], axis=0)
+
+        def max_f64(_ctx, buf, n):
+            v = np.ctypeslib.as_array(buf, (n,))
+            parts = self.impl.allgather_bytes(v.tobytes())
+            v[:] = np.max([np.frombuffer(b, np.float64) for b in parts], axis=0)
+
+        def gather(_ctx, send, recv, nbytes):
+            mine = C.string_at(send, nbytes) if nbytes else b""
+            parts = self.impl.allgather_bytes(mine)
+            out = b"".join(parts)
+            if out:
+                C.memmove(recv, out, len(out))
+
+        self._cbs = (ALLRED_I64(guard(sum_i64)), ALLRED_U64(guard(max_u64)),
+                     ALLRED_F64(guard(max_f64)), ALLGATHER(guard(gather)))
+        self.c = SwHostComm(None, *self._cbs)
+
+
+class TorchGroupComm:
+    """allgather_bytes over a torch.distributed process group (gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def allgather_bytes(self, data: bytes):
+        import torch
+
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else \
+            torch.zeros(0, dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [o.numpy().tobytes() for o in out]
+
+
+def shard_range(total_jobs: int, world: int, rank: int):
+    """sw_dist_shard_range in Python (the same rule, for callers that slice)."""
+    if world < 1 or 512 % world or not 0 <= rank < world or total_jobs < 0:
+        raise ValueError("world must divide 512 and 0 <= rank < world")
+    q = (total_jobs + 511) // 512
+    per = (512 // world) * q
+    return min(total_jobs, rank * per), min(total_jobs, (rank + 1) * per)
+
+
 def log_bases(bases):
     """shockwave.py:99-105 — log(β_b), with log(0) replaced by log(1e-6)."""
     return [math.log(1e-6) if b == 0.0 else math.log(b) for b in bases]
@@ -135,6 +231,12 @@ class ProblemArrays:
         p.priority = self.p.ctypes.data_as(_dp)
         return p
 
+    def slice(self, lo: int, hi: int) -> "ProblemArrays":
+        """This instance's jobs [lo, hi) with the global scalars (a rank's shard)."""
+        return ProblemArrays(self.w[lo:hi], self.d[lo:hi], self.F[lo:hi], self.E[lo:hi],
+                             self.R[lo:hi], self.p[lo:hi], self.T, self.G, self.delta, self.k,
+                             tuple(self.bases))
+
     def c_result(self) -> SwResult:
         r = SwResult()
         r.plan = self.plan.ctypes.data_as(_up)
@@ -171,7 +273,8 @@ EXPORTED_SYMBOLS = (
     "sw_abi_version", "sw_create", "sw_destroy", "sw_last_error", "sw_create_error",
     "sw_plan_solve", "sw_plan_solve_batch", "sw_batch_upload", "sw_batch_run",
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
-    "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve",
+    "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
+    "sw_dist_init_host",
 )
 
 
@@ -226,6 +329,11 @@ def load(path: str | None = None):
     lib.sw_dist_plan_solve.argtypes = [C.c_void_p, C.POINTER(SwProblem), C.c_int64, C.c_int64,
                                        C.POINTER(SwResult)]
     lib.sw_dist_plan_solve.restype = C.c_int
+    lib.sw_dist_shard_range.argtypes = [C.c_int64, C.c_int32, C.c_int32,
+                                        C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    lib.sw_dist_shard_range.restype = C.c_int
+    lib.sw_dist_init_host.argtypes = [C.c_void_p, C.POINTER(SwHostComm), C.c_int32, C.c_int32]
+    lib.sw_dist_init_host.restype = C.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -304,3 +412,36 @@ class Solver:
         self._check(self.lib.sw_kernel_times(self.h, C.byref(a), C.byref(b), C.byref(n)),
                     "sw_kernel_times")
         return a.value, b.value, n.value
+
+    # ---- sharded single instance (include/shockwave_amd.h sw_dist_*) ----
+    def dist_init(self, unique_id: bytes, rank: int, world: int):
+        """RCCL collectives; unique_id from unique_id() on rank 0, broadcast by the caller."""
+        buf = C.create_string_buffer(bytes(unique_id), SW_NCCL_UNIQUE_ID_BYTES)
+        self._check(self.lib.sw_dist_init(self.h, buf, int(rank), int(world)), "sw_dist_init")
+
+    def dist_init_host(self, comm: "HostComm", rank: int, world: int):
+        """Host collectives (e.g. gloo through TorchGroupComm)."""
+        self._comm = comm  # keeps the callbacks alive
+        self._check(self.lib.sw_dist_init_host(self.h, C.byref(comm.c), int(rank), int(world)),
+                    "sw_dist_init_host")
+
+    def dist_solve(self, local: ProblemArrays, job_offset: int, total_jobs: int) -> dict:
+        prob = local.c_problem()
+        res = local.c_result()
+        rc = self.lib.sw_dist_plan_solve(self.h, C.byref(prob), int(job_offset), int(total_jobs),
+                                         C.byref(res))
+        comm = getattr(self, "_comm", None)
+        if rc < 0 and comm is not None and comm.error is not None:
+            raise NativeError(f"sw_dist_plan_solve: collective failed: {comm.error!r}")
+        self._check(rc, "sw_dist_plan_solve")
+        return result_dict(res, local, rc)
+
+
+def unique_id(lib=None) -> bytes:
+    """sw_dist_unique_id (call on rank 0 only)."""
+    lib = lib or load()
+    buf = C.create_string_buffer(SW_NCCL_UNIQUE_ID_BYTES)
+    rc = lib.sw_dist_unique_id(buf)
+    if rc < 0:
+        raise NativeError(f"sw_dist_unique_id failed ({rc})")
+    return buf.raw

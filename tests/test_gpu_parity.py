@@ -39,6 +39,17 @@ def test_gpu_matches_twin(case, gpu_solver, twin):
     assert_same_result(rg, rt, f"case {case}")
 
 
+@pytest.mark.parametrize("wide", [16, 32, 200])
+def test_gpu_wide_jobs_match_twin(wide, gpu_solver, twin):
+    """Jobs of width ≥ 16 (the round loop's width tail once packed w in 4 bits)."""
+    a = ss.synth_problem(21, 300, 512, 20, 120.0, 1e1, 5.0)
+    a.w[::7] = wide
+    a.w[::11] = 3
+    rg = gpu_solver.solve(a)
+    check_plan_valid(a, rg)
+    assert_same_result(rg, twin.solve(a), f"wide={wide}")
+
+
 def test_gpu_large_instance_workspace_path(gpu_solver, twin):
     """N > 1024 takes the HBM-workspace path of the kernel."""
     a = ss.synth_problem(42, 2500, 700, 30, 120.0, 1e5, 5.0)

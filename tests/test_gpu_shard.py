@@ -1,0 +1,95 @@
+"""Sharded single-instance solve on the GPU engine (csrc/sw_shard.hip).
+
+The box has one MI355X, so multi-rank runs put W handles on cuda:0 as threads
+of this process with host collectives (a barrier-based allgather); the
+world-1 run goes through RCCL (ncclAllReduce / ncclAllGather on the handle's
+stream).  Every run must return exactly the single-instance result of the CPU
+twin (oracle/plan_twin.c) — which the batched GPU kernel also matches — for
+plan rows, counts and the bits of every objective.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import sw_native as sn
+import sw_synth as ss
+from helpers import check_plan_valid
+from test_shard import CASES, ThreadGroup, assemble, assert_same_as_single
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_shard_threads(a, world):
+    group = ThreadGroup(world)
+    out = [None] * world
+    errs = []
+
+    def work(r):
+        try:
+            s = sn.Solver(device=0)
+            s.dist_init_host(sn.HostComm(group.member(r)), r, world)
+            lo, hi = sn.shard_range(a.N, world, r)
+            out[r] = (lo, hi, s.dist_solve(a.slice(lo, hi), lo, a.N))
+            s.close()
+        except Exception as e:
+            errs.append(e)
+            group.barrier.abort()
+
+    ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    return assemble(a, out)
+
+
+@pytest.fixture(scope="module")
+def rccl_solver():
+    s = sn.Solver(device=0)
+    s.dist_init(sn.unique_id(), 0, 1)
+    yield s
+    s.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"N{c[1]}_G{c[2]}_T{c[3]}_k{c[4]:g}" for c in CASES])
+def test_gpu_shard_rccl_world1(case, rccl_solver, twin):
+    seed, N, G, T, k, lam = case
+    a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+    r = rccl_solver.dist_solve(a, 0, a.N)
+    check_plan_valid(a, r)
+    assert_same_as_single(r, twin.solve(a), f"rccl W=1 {case}")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("case", [CASES[1], CASES[4], CASES[6], CASES[7]],
+                         ids=["N50", "N300_T64", "N900", "N1500"])
+def test_gpu_shard_host_comm(case, world, twin):
+    seed, N, G, T, k, lam = case
+    a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+    r = gpu_shard_threads(a, world)
+    check_plan_valid(a, r)
+    assert_same_as_single(r, twin.solve(a), f"W={world} {case}")
+
+
+def test_gpu_shard_c4_shape(rccl_solver, twin):
+    """The 10k-job × 30-round C4 instance, whole on one rank."""
+    c = ss.C4
+    a = ss.synth_problem(11, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
+    r = rccl_solver.dist_solve(a, 0, a.N)
+    check_plan_valid(a, r)
+    assert_same_as_single(r, twin.solve(a), "C4")
+
+
+def test_gpu_shard_c4_world8(twin):
+    c = ss.C4
+    a = ss.synth_problem(12, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
+    r = gpu_shard_threads(a, 8)
+    assert_same_as_single(r, twin.solve(a), "C4 W=8")
+
+
+def test_gpu_shard_rejects_bad_slice(rccl_solver):
+    a = ss.synth_problem(0, 100, 32, 10, 120.0, 1e5, 5.0)
+    with pytest.raises(sn.NativeError):
+        rccl_solver.dist_solve(a.slice(0, 50), 0, a.N)

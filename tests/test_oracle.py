@@ -108,6 +108,8 @@ def test_job_wider_than_cluster_never_scheduled(twin):
     r = twin.solve(a)
     assert r["planned_rounds"][0] == 0
     check_plan_valid(a, r)
+    a = _arr(nworkers=[1000, 1], num_gpus=2)  # any width is accepted if it never fits
+    assert twin.solve(a)["planned_rounds"][0] == 0
 
 
 def test_zero_regularizer_maximises_utility(twin):
@@ -129,6 +131,7 @@ def test_finished_job_and_zero_priority(twin):
     dict(nworkers=[0, 1]), dict(total_epochs=[0, 4]), dict(completed_epochs=[11, 1]),
     dict(epoch_duration=[0.0, 1.0]), dict(priority=[-1.0, 1.0]),
     dict(priority=[float("nan"), 1.0]), dict(regularizer=-1.0), dict(future_rounds=65),
+    dict(nworkers=[256, 1], num_gpus=300),  # schedulable but wider than SW_MAX_WIDTH
 ])
 def test_invalid_inputs_rejected(bad, twin):
     a = _arr(**bad)

@@ -1,0 +1,224 @@
+"""Sharded single-instance solve (include/shockwave_amd.h sw_dist_*).
+
+The controller (csrc/sw_shard_ctl.h) runs here on the CPU shard engine
+(oracle/shard_twin.c) with W ranks as threads (a barrier-based allgather) and,
+for the multi-process path, as W=2 processes over torch.distributed gloo.
+The bar: for every world size W | 512 the sharded solve returns exactly the
+single-instance result of the twin (oracle/plan_twin.c), which the GPU kernel
+matches bit for bit (tests/test_gpu_parity.py) — plan rows, counts and the
+bits of every objective.  Only `iters` differs (it counts collective steps).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import sw_native as sn
+import sw_synth as ss
+from conftest import TWIN_SO, _build_twin
+from helpers import check_plan_valid
+
+SCALARS = ("objective", "utility", "makespan", "p2_objective", "bound")
+
+
+class ThreadGroup:
+    """W ranks as threads of this process: allgather through shared slots."""
+
+    def __init__(self, world):
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.slots = [None] * world
+
+    def member(self, rank):
+        group = self
+
+        class Member:
+            def allgather_bytes(self, data):
+                group.slots[rank] = data
+                group.barrier.wait()
+                out = list(group.slots)
+                group.barrier.wait()
+                return out
+
+        return Member()
+
+
+@pytest.fixture(scope="module")
+def shard_lib():
+    _build_twin()
+    lib = ctypes.CDLL(TWIN_SO)
+    lib.shard_twin_solve.argtypes = [ctypes.POINTER(sn.SwHostComm), ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.POINTER(sn.SwProblem), ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(sn.SwResult)]
+    lib.shard_twin_solve.restype = ctypes.c_int
+    return lib
+
+
+def shard_solve_rank(lib, comm, rank, world, a):
+    lo, hi = sn.shard_range(a.N, world, rank)
+    loc = a.slice(lo, hi)
+    pr, res = loc.c_problem(), loc.c_result()
+    rc = lib.shard_twin_solve(ctypes.byref(comm.c), rank, world, ctypes.byref(pr), lo, a.N,
+                              ctypes.byref(res))
+    return lo, hi, sn.result_dict(res, loc, rc)
+
+
+def run_threads(lib, a, world):
+    group = ThreadGroup(world)
+    out = [None] * world
+    errs = []
+
+    def work(r):
+        try:
+            comm = sn.HostComm(group.member(r))
+            out[r] = shard_solve_rank(lib, comm, r, world, a)
+        except Exception as e:  # pragma: no cover - surfaced below
+            errs.append(e)
+            group.barrier.abort()
+
+    ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    return assemble(a, out)
+
+
+def assemble(a, parts):
+    plan = np.zeros((a.N, a.T), np.uint8)
+    cnt = np.zeros(a.N, np.int32)
+    r0 = parts[0][2]
+    for lo, hi, r in parts:
+        assert r["rc"] >= 0, r["rc"]
+        for key in SCALARS + ("status", "rc", "iters"):
+            assert np.float64(r[key]).tobytes() == np.float64(r0[key]).tobytes(), key
+        plan[lo:hi] = r["plan"]
+        cnt[lo:hi] = r["planned_rounds"]
+    return dict(r0, plan=plan, planned_rounds=cnt)
+
+
+def assert_same_as_single(rs, rt, what):
+    assert rs["status"] == rt["status"], what
+    assert rs["rc"] == rt["rc"], what
+    assert np.array_equal(rs["planned_rounds"], rt["planned_rounds"]), f"{what}: counts"
+    assert np.array_equal(rs["plan"], rt["plan"]), f"{what}: plan"
+    for key in SCALARS:
+        assert np.float64(rs[key]).tobytes() == np.float64(rt[key]).tobytes(), \
+            f"{what}: {key} {rs[key]!r} vs {rt[key]!r}"
+
+
+CASES = [
+    # (seed, N, G, T, k, lam)
+    (0, 12, 4, 6, 1e5, 5.0),
+    (1, 50, 32, 20, 1e-3, 15.0),
+    (2, 120, 64, 20, 1e-3, 15.0),
+    (3, 120, 128, 20, 1e1, 5.0),
+    (4, 300, 64, 64, 1e1, 5.0),
+    (5, 200, 32, 40, 0.5, 3.0),
+    (6, 900, 256, 30, 1e5, 5.0),
+    (7, 1500, 400, 30, 1e5, 5.0),
+    (8, 40, 8, 10, 0.0, 5.0),
+    (9, 30, 6, 12, 1e2, 5.0),
+]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("case", CASES, ids=[f"N{c[1]}_G{c[2]}_T{c[3]}_k{c[4]:g}" for c in CASES])
+def test_sharded_equals_single(case, world, shard_lib, twin):
+    seed, N, G, T, k, lam = case
+    a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+    rs = run_threads(shard_lib, a, world)
+    rt = twin.solve(a)
+    check_plan_valid(a, rs)
+    assert_same_as_single(rs, rt, f"W={world} case {case}")
+
+
+def test_sharded_edge_cases(shard_lib, twin):
+    # empty instance; jobs wider than the cluster; one job; all-equal jobs (ties)
+    a0 = ss.synth_problem(1, 0, 8, 5, 120.0, 1e5, 5.0)
+    rs = run_threads(shard_lib, a0, 2)
+    assert rs["status"] & sn.SW_STATUS_NO_PLANNED
+    a = ss.synth_problem(2, 64, 4, 10, 120.0, 1e2, 5.0)
+    a.w[::3] = 8  # wider than G=4: never schedulable
+    assert_same_as_single(run_threads(shard_lib, a, 4), twin.solve(a), "wide jobs")
+    a1 = ss.synth_problem(3, 1, 8, 5, 120.0, 1e5, 5.0)
+    assert_same_as_single(run_threads(shard_lib, a1, 8), twin.solve(a1), "one job")
+    at = ss.synth_problem(4, 96, 16, 8, 120.0, 1e1, 5.0)
+    for arr in (at.w, at.d, at.F, at.E, at.R, at.p):
+        arr[:] = arr[0]
+    assert_same_as_single(run_threads(shard_lib, at, 4), twin.solve(at), "ties")
+
+
+def test_shard_range_rule():
+    for N in (0, 1, 511, 512, 513, 10_000):
+        for W in (1, 2, 8, 512):
+            spans = [sn.shard_range(N, W, r) for r in range(W)]
+            assert spans[0][0] == 0 and spans[-1][1] == N
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b
+    with pytest.raises(ValueError):
+        sn.shard_range(100, 3, 0)
+
+
+def test_shard_rejects_wrong_slice(shard_lib):
+    a = ss.synth_problem(0, 100, 32, 10, 120.0, 1e5, 5.0)
+    group = ThreadGroup(1)
+    comm = sn.HostComm(group.member(0))
+    loc = a.slice(0, 50)  # W=1 must hold every job
+    pr, res = loc.c_problem(), loc.c_result()
+    rc = shard_lib.shard_twin_solve(ctypes.byref(comm.c), 0, 1, ctypes.byref(pr), 0, a.N,
+                                    ctypes.byref(res))
+    assert rc == sn.SW_ERR_INVALID
+
+
+# ---- multi-process: world_size 2 over torch.distributed gloo ----------------
+
+def _gloo_worker(rank, world, port, outdir, cases):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = ctypes.CDLL(TWIN_SO)
+    lib.shard_twin_solve.argtypes = [ctypes.POINTER(sn.SwHostComm), ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.POINTER(sn.SwProblem), ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(sn.SwResult)]
+    lib.shard_twin_solve.restype = ctypes.c_int
+    comm = sn.HostComm(sn.TorchGroupComm())
+    for ci, case in enumerate(cases):
+        seed, N, G, T, k, lam = case
+        a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+        lo, hi, r = shard_solve_rank(lib, comm, rank, world, a)
+        np.savez(os.path.join(outdir, f"c{ci}_r{rank}.npz"), lo=lo, hi=hi, plan=r["plan"],
+                 cnt=r["planned_rounds"],
+                 scal=np.array([r[k] for k in SCALARS], dtype=np.float64),
+                 meta=np.array([r["rc"], r["status"], r["iters"]], dtype=np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_gloo_world2(tmp_path, twin):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cases = [CASES[1], CASES[6], CASES[7]]
+    mp.spawn(_gloo_worker, args=(2, port, str(tmp_path), cases), nprocs=2, join=True)
+    for ci, case in enumerate(cases):
+        seed, N, G, T, k, lam = case
+        a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+        parts = []
+        for r in range(2):
+            z = np.load(tmp_path / f"c{ci}_r{r}.npz")
+            res = {key: float(v) for key, v in zip(SCALARS, z["scal"])}
+            res.update(rc=int(z["meta"][0]), status=int(z["meta"][1]), iters=int(z["meta"][2]),
+                       plan=z["plan"], planned_rounds=z["cnt"])
+            parts.append((int(z["lo"]), int(z["hi"]), res))
+        rs = assemble(a, parts)
+        assert_same_as_single(rs, twin.solve(a), f"gloo case {case}")
