@@ -7,8 +7,15 @@
  * (position p = E·tid + i), so a block exclusive scan is the twin's running
  * "excl" over positions.  Per-position state is packed in a VGPR:
  * r (rounds still to place, 8 bits) | w << 8 (width, 8 bits) | sel << 16.
- * Per-round histograms live in LDS and are double-buffered by round parity,
- * so each round needs one barrier before its tiers.
+ *
+ * The width histogram over remaining rounds, Hu[v] = Σ w over positions with
+ * r = v, is built once and then kept up to date: a position placed in round t
+ * moves w from Hu[r] to Hu[r − 1] (2 LDS atomics per placed position instead
+ * of one per position per round — the per-round rebuild was the kernel's LDS
+ * bank-conflict hot spot at 10k jobs).  The round's clamped histogram
+ * H[v] = Hu[v] (v < R), H[R] = Σ_{v ≥ R} Hu[v] is formed in registers.  The
+ * tier histogram SH is per round and double-buffered by round parity, so
+ * each round needs one barrier before its tiers.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -16,11 +23,30 @@
 
 #include "sw_block.h"
 
+#ifdef SW_STAMPS
+/* diagnostic builds: cycles per round-loop phase, thread 0's view
+ * (0 setup, 1 histogram+need, 2 tiers, 3 fill, 4 tail, 5 apply) */
+__device__ uint64_t g_sw_pack_stamps[8];
+#define SWP_STAMP(k)                                                            \
+    do {                                                                        \
+        if (threadIdx.x == 0) {                                                 \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();                 \
+            atomicAdd((unsigned long long*)&g_sw_pack_stamps[k], now_ - swp_t_); \
+            swp_t_ = now_;                                                      \
+        }                                                                       \
+    } while (0)
+#else
+#define SWP_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t pk_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t pk_w(uint32_t s) { return (s >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t pk_sel(uint32_t s) { return (s >> 16) & 1u; }
 
-/* LDS the round loop needs: two 68-entry buffers each for H and SH. */
+/* LDS the round loop needs: the running histogram Hu (H[0]); the rest is
+ * spare (kept for the carve-up of sw_kernels.hip). */
 struct sw_pack_lds {
     int32_t H[2][68];
     int32_t SH[2][68];
@@ -31,115 +57,136 @@ struct sw_pack_lds {
  * st[i] holds position E·tid + i's packed state (0 past A); on return mk[i]
  * has bit t set when that position runs in round t and st[i]'s r field is
  * what could not be placed.
+ *
+ * Tiers (twin: the m loop of pack).  Tier m may take positions with rr > m
+ * up to q = need[m] − red(m), red(m) = Σ_{v>m} SH[v] the width already taken
+ * by this round's tiers with rr = v.  Tiers run from high m down and every
+ * position a tier m' took has rr > m' > m, so red(m) is simply the running
+ * total of tier takes: no per-round SH histogram is needed.
+ *
+ * The per-position loops are branch-free (predicated adds and selects): with
+ * E up to 32 positions per thread, per-position branches each held a 64-bit
+ * exec mask and spilled the SGPR file.
  */
 template <int E>
 __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int A, int T, int G,
                                                uint32_t (&st)[E], uint64_t (&mk)[E]) {
     const int tid = threadIdx.x;
     const int lane = lane_id();
-    if (tid < 68) { L->H[0][tid] = 0; L->SH[0][tid] = 0; }
+#ifdef SW_STAMPS
+    uint64_t swp_t_ = __builtin_amdgcn_s_memtime();
+#endif
+    /* positions past A carry st = 0 (r = 0, w = 0): they fail every
+     * eligibility test below, so no per-position bound check is needed */
+    int32_t* Hu = L->H[0];
+    if (tid < 68) Hu[tid] = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) mk[i] = 0;
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+        if (st[i] != 0u) atomicAdd(&Hu[pk_r(st[i])], (int32_t)pk_w(st[i]));
+    SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
-        int32_t* Hc = L->H[t & 1];
-        int32_t* SHc = L->SH[t & 1];
         int32_t cap = G;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-            if (E * tid + i < A) {
-                const int rr = (int)pk_r(st[i]) < R ? (int)pk_r(st[i]) : R;
-                atomicAdd(&Hc[rr], (int32_t)pk_w(st[i]));
-            }
-        }
-        /* clear next round's buffers (read by nobody this round) */
-        if (tid < 68) { L->H[(t + 1) & 1][tid] = 0; L->SH[(t + 1) & 1][tid] = 0; }
-        __syncthreads();
+        __syncthreads(); /* Hu holds the placements of round t − 1 */
+        /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
+         * lane m holds hv = H[m + 1] */
+        const int32_t suf = wave_sufscan_i32(Hu[lane]);
+        const int32_t tailR = (R < 64 ? __shfl(suf, R, 64) : 0) + Hu[64];
+        const int32_t hv = (lane + 1 < R) ? Hu[lane + 1] : (lane + 1 == R ? tailR : 0);
         /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
-        const int32_t hv = (lane + 1 <= R) ? Hc[lane + 1] : 0;
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
         const int32_t need = (lane < R) ? (S1 - lane * S0) - G * (R - 1 - lane) : -1;
+        SWP_STAMP(1);
         /* tiers: jobs with more than m rounds left must shed enough now */
         int mstart = R - 1;
+        int32_t red = 0;
         while (mstart >= 0) {
-            const int32_t shv = (lane + 1 <= R) ? SHc[lane + 1] : 0;
-            const int32_t red = wave_sufscan_i32(shv);
             const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
             if (mask == 0) break;
             const int m = 63 - __builtin_clzll(mask);
-            const int32_t q = __shfl(need - red, m, 64);
+            const int32_t q = __shfl(need, m, 64) - red;
             int32_t lt = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
-                const int rr = (int)pk_r(st[i]) < R ? (int)pk_r(st[i]) : R;
-                if (E * tid + i < A && !pk_sel(st[i]) && rr > m) lt += (int32_t)pk_w(st[i]);
+                const int rr = min((int)pk_r(st[i]), R);
+                lt += (!pk_sel(st[i]) && rr > m) ? (int32_t)pk_w(st[i]) : 0;
             }
             int32_t tot;
             int32_t ex = blk.exscan(lt, tot);
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
-                const int rr = (int)pk_r(st[i]) < R ? (int)pk_r(st[i]) : R;
-                if (E * tid + i < A && !pk_sel(st[i]) && rr > m) {
-                    const int32_t w = (int32_t)pk_w(st[i]);
-                    if (ex < q && ex + w <= cap) {
-                        st[i] |= (1u << 16);
-                        atomicAdd(&SHc[rr], w);
-                        took += w;
-                    }
-                    ex += w;
-                }
+                const int rr = min((int)pk_r(st[i]), R);
+                const int32_t w = (int32_t)pk_w(st[i]);
+                const bool elig = !pk_sel(st[i]) && rr > m;
+                const bool take = elig && ex < q && ex + w <= cap;
+                st[i] |= take ? (1u << 16) : 0u;
+                took += take ? w : 0;
+                ex += elig ? w : 0;
             }
-            cap -= blk.sum32(took);
+            took = blk.sum32(took);
+            cap -= took;
+            red += took;
             mstart = m - 1;
         }
+        SWP_STAMP(2);
         /* fill the rest of the round in order */
         {
             int32_t lt = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i)
-                if (E * tid + i < A && !pk_sel(st[i]) && pk_r(st[i]) > 0) lt += (int32_t)pk_w(st[i]);
+                lt += (!pk_sel(st[i]) && pk_r(st[i]) > 0) ? (int32_t)pk_w(st[i]) : 0;
             int32_t tot;
             int32_t ex = blk.exscan(lt, tot);
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
-                if (E * tid + i < A && !pk_sel(st[i]) && pk_r(st[i]) > 0) {
-                    const int32_t w = (int32_t)pk_w(st[i]);
-                    if (ex + w <= cap) { st[i] |= (1u << 16); took += w; }
-                    ex += w;
-                }
+                const int32_t w = (int32_t)pk_w(st[i]);
+                const bool elig = !pk_sel(st[i]) && pk_r(st[i]) > 0;
+                const bool take = elig && ex + w <= cap;
+                st[i] |= take ? (1u << 16) : 0u;
+                took += take ? w : 0;
+                ex += elig ? w : 0;
             }
             cap -= blk.sum32(took);
         }
+        SWP_STAMP(3);
         /* width tail: first position in order that still fits; the key
          * carries (position << 8 | w) so the min also names the width */
         while (cap > 0) {
             int32_t best = 0x7FFFFFFF;
 #pragma unroll
             for (int i = E - 1; i >= 0; --i) {
-                if (E * tid + i < A && !pk_sel(st[i]) && pk_r(st[i]) > 0 && (int32_t)pk_w(st[i]) <= cap)
-                    best = ((E * tid + i) << 8) | (int32_t)pk_w(st[i]);
+                const bool ok = !pk_sel(st[i]) && pk_r(st[i]) > 0 &&
+                                (int32_t)pk_w(st[i]) <= cap;
+                best = ok ? (((E * tid + i) << 8) | (int32_t)pk_w(st[i])) : best;
             }
             best = blk.min32(best);
             if (best == 0x7FFFFFFF) break;
             const int pos = best >> 8;
-            if (pos / E == tid) {
 #pragma unroll
-                for (int i = 0; i < E; ++i)
-                    if (i == pos % E) st[i] |= (1u << 16);
-            }
+            for (int i = 0; i < E; ++i) st[i] |= (E * tid + i == pos) ? (1u << 16) : 0u;
             cap -= best & 0xFF;
         }
+        SWP_STAMP(4);
+        /* apply (all reads of Hu this round happened before the fill's
+         * barrier): placed positions move their width down one bin */
 #pragma unroll
         for (int i = 0; i < E; ++i) {
-            if (E * tid + i < A && pk_sel(st[i])) {
-                mk[i] |= (1ull << t);
-                st[i] = (st[i] & 0xFF00u) | (pk_r(st[i]) - 1u);
+            const bool sel = pk_sel(st[i]) != 0; /* only existing positions get selected */
+            const uint32_t r = pk_r(st[i]);
+            mk[i] |= sel ? (1ull << t) : 0ull;
+            st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
+            if (sel) {
+                atomicAdd(&Hu[r], -(int32_t)pk_w(st[i]));
+                atomicAdd(&Hu[r - 1], (int32_t)pk_w(st[i]));
             }
         }
+        SWP_STAMP(5);
     }
     __syncthreads();
 }

@@ -23,13 +23,14 @@
  * rank; DESIGN.md §7 has the per-step budget):
  *   k_force / k_take / k_between / k_tail_best   thread per job, binary
  *        searches on the monotone g and key rows, wave reductions + atomics
- *   k_count / k_feasible   thread per (job, round) element: one binary
- *        search over the ≤63 sorted thresholds, an LDS histogram, a suffix
- *        sum on the host — K price/level probes per pass (K-ary search)
+ *   k_probe    thread per (job, round) item: one binary search over the ≤63
+ *        ascending thresholds, an LDS histogram, a suffix sum on the host —
+ *        K price/level probes per pass (K-ary search)
  *   k_assign   one workgroup: the job-ordered tie group as a block scan
- *   k_eval     one workgroup, thread per deterministic-sum lane (sw_detsum's
- *        left-to-right chunks), so the gathered lanes reproduce the
- *        single-instance sums bit for bit
+ *   k_eval_jobs / k_eval_lanes   per-job values (thread per job), then one
+ *        workgroup sums each deterministic-sum lane left to right (sw_detsum's
+ *        chunks), so the gathered lanes reproduce the single-instance sums
+ *        bit for bit
  *   k_pack_rank / k_pack_rounds   the placement (sw_pack.h)
  */
 #include <hip/hip_runtime.h>
@@ -72,6 +73,8 @@ struct ShardDev {
     const double* p;
     int32_t* l;
     int32_t* taken;
+    int32_t* tie; /* w·(count(key ≥ ρ) − taken), stored by k_take */
+    double* xa;   /* per-job values of the last reduction (two rows of NL) */
     int32_t* arr[SW_A_COUNT];
     uint64_t* y[SW_Y_COUNT];
     uint8_t* plan;
@@ -174,8 +177,9 @@ __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf)
     red_add(S.red + 1, wall);
 }
 
-/* K probes at once: element (job, n) adds w to bin #{m : thr_m < v}; the
- * count for probe m is the suffix Σ_{b > m} bin[b] (host side). */
+/* K probes at once: item (job, n) adds w to bin #{m : thr_m < v(n)} (v =
+ * the key, or g for the level probes); the count for probe m is the suffix
+ * Σ_{b > m} bin[b] (host side).  Thread per item: the whole grid is busy. */
 template <bool LEVEL>
 __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
     __shared__ int32_t bins[SW_SHARD_K + 1];
@@ -247,41 +251,42 @@ __global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
         S.taken[i] = tk;
         wt = (long long)c.w * tk;
         tie = (long long)c.w * (key_count<true>(row, l, tj, rho) - tk);
+        S.tie[i] = (int32_t)tie;
     }
     red_add(S.red + 0, wt);
     red_add(S.red + 1, tie);
 }
 
-/* tie group in job order: one workgroup, thread t owns a contiguous chunk */
-__global__ __launch_bounds__(SW_BLOCK) void k_assign(ShardDev S, uint32_t rho, long long rem,
-                                                     long long excl0) {
-    __shared__ long long wsum[SW_WAVES];
-    const int tid = threadIdx.x;
-    const int per = (S.NL + SW_BLOCK - 1) / SW_BLOCK;
-    const int lo = tid * per, hi = min(S.NL, lo + per);
-    long long mine = 0;
-    for (int i = lo; i < hi; ++i) {
-        const sw_jobc c = S.jc[i];
-        const int tie = key_count<true>(S.keys + (size_t)i * S.T, S.l[i], tj_of(S, c), rho) - S.taken[i];
-        mine += (long long)c.w * tie;
-    }
-    const long long inc = wave_incscan(mine);
-    if (lane_id() == 63) wsum[wave_id()] = inc;
-    __syncthreads();
-    long long base = excl0;
-    for (int w = 0; w < wave_id(); ++w) base += wsum[w];
-    long long excl = base + inc - mine, used = 0;
-    for (int i = lo; i < hi; ++i) {
-        const sw_jobc c = S.jc[i];
-        const int tie = key_count<true>(S.keys + (size_t)i * S.T, S.l[i], tj_of(S, c), rho) - S.taken[i];
-        const long long wj = c.w;
-        int tt;
-        if (excl + wj * tie <= rem) tt = tie;
-        else if (excl <= rem) tt = (int)((rem - excl) / wj);
-        else tt = 0;
-        S.arr[SW_A_N][i] = S.l[i] + S.taken[i] + tt;
-        used += wj * tt;
-        excl += wj * tie;
+/* tie group in job order (twin: the excl loop of select_level): one
+ * workgroup walks the jobs in coalesced tiles of SW_BLOCK, a block scan per
+ * tile, the running prefix carried across tiles */
+__global__ __launch_bounds__(SW_BLOCK) void k_assign(ShardDev S, long long rem, long long excl0) {
+    __shared__ long long wsum[2][SW_WAVES];
+    long long carry = excl0, used = 0;
+    int par = 0;
+    for (int base = 0; base < S.NL; base += SW_BLOCK, par ^= 1) {
+        const int i = base + (int)threadIdx.x;
+        const long long t = i < S.NL ? (long long)S.tie[i] : 0;
+        const long long inc = wave_incscan(t);
+        if (lane_id() == 63) wsum[par][wave_id()] = inc;
+        __syncthreads();
+        long long before = 0, tot = 0;
+        for (int w = 0; w < SW_WAVES; ++w) {
+            before += w < wave_id() ? wsum[par][w] : 0;
+            tot += wsum[par][w];
+        }
+        if (i < S.NL) {
+            const long long excl = carry + before + inc - t;
+            const long long wj = S.jc[i].w;
+            const int tie = (int)(t / wj);
+            int tt;
+            if (excl + t <= rem) tt = tie;
+            else if (excl <= rem) tt = (int)((rem - excl) / wj);
+            else tt = 0;
+            S.arr[SW_A_N][i] = S.l[i] + S.taken[i] + tt;
+            used += wj * tt;
+        }
+        carry += tot;
     }
     red_add(S.red + 0, used);
 }
@@ -303,77 +308,89 @@ __global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
 
 /* ---- reductions with deterministic lane sums ------------------------------- */
 
-/* Thread ℓ < LW owns deterministic-sum lane rank·LW + ℓ (jobs [L·q, L·q+q)).
- * Writes [A lanes][B lanes][gm bits][isum] to out. */
-__global__ __launch_bounds__(SW_BLOCK) void k_eval(ShardDev S, int sel, int arg, double* out) {
-    __shared__ uint64_t sg[SW_WAVES];
-    __shared__ long long ss[SW_WAVES];
-    const int lane = threadIdx.x;
+/* Per-job values of a reduction step: xa[i] (A row), xa[NL + i] (B row);
+ * red[0] = max g (bits), red[1] = integer sum.  SW_EV_FINAL also writes the
+ * plan row and count of job i. */
+__global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const int32_t* arr,
+                                                   const uint64_t* ysrc) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
     double fa = 0.0, fb = 0.0, gm = 0.0;
     long long is = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        if (sel == SW_EV_SELECT) {
+            const int n = S.arr[SW_A_N][i];
+            fa = sw_f(&c, n, S.nb, S.beta, S.ell);
+            fb = sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell);
+            gm = sw_g(&c, n);
+        } else if (sel == SW_EV_GMAX) {
+            gm = sw_g(&c, arr[i]);
+        } else if (sel == SW_EV_PACKED) {
+            const int pl = arr[i];
+            fa = sw_f(&c, pl, S.nb, S.beta, S.ell);
+            gm = sw_g(&c, pl);
+            is = (long long)c.w * (S.arr[SW_A_NB][i] - pl);
+        } else if (sel == SW_EV_P2OK) {
+            is = S.arr[SW_A_PL][i] != S.arr[SW_A_NFIN][i];
+        } else { /* SW_EV_FINAL */
+            const uint64_t m = ysrc[i];
+            const int cn = __popcll(m);
+            long long Ssum = 0;
+            uint8_t* row = S.plan + (size_t)i * S.T;
+            for (int t = 0; t < S.T; ++t) {
+                const uint32_t bit = (uint32_t)((m >> t) & 1ull);
+                Ssum += bit ? t : 0;
+                row[t] = (uint8_t)bit;
+            }
+            S.planned[i] = cn;
+            fa = sw_f(&c, cn, S.nb, S.beta, S.ell);
+            fb = cn > 0 ? ((double)Ssum / (double)cn) * S.p[i] : 0.0;
+            gm = sw_g(&c, cn);
+            is = cn > 0;
+        }
+        S.xa[i] = fa;
+        S.xa[(size_t)S.NL + i] = fb;
+    }
+    red_umax(S.red + 0, sw_bits(gm)); /* g ≥ 0: bit order = value order */
+    red_add(S.red + 1, is);
+}
+
+/* Thread ℓ < LW owns deterministic-sum lane rank·LW + ℓ: the left-to-right
+ * sum of its jobs [L·q, L·q + q) (sw_detsum), for both rows.
+ * Writes [A lanes][B lanes][gm][isum] to out. */
+__global__ __launch_bounds__(SW_BLOCK) void k_eval_lanes(ShardDev S, double* out) {
+    const int lane = threadIdx.x;
     if (lane < S.LW) {
         const int64_t L = (int64_t)S.rank * S.LW + lane;
         const int64_t j0 = L * S.q, j1 = min(S.N, j0 + S.q);
+        double fa = 0.0, fb = 0.0;
+        const double* xa = S.xa - S.off;
+        const double* xb = S.xa + S.NL - S.off;
+#pragma unroll 4
         for (int64_t j = j0; j < j1; ++j) {
-            const int i = (int)(j - S.off);
-            const sw_jobc c = S.jc[i];
-            if (sel == SW_EV_SELECT) {
-                const int n = S.arr[SW_A_N][i];
-                fa = fa + sw_f(&c, n, S.nb, S.beta, S.ell);
-                fb = fb + sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell);
-                gm = sw_max(gm, sw_g(&c, n));
-            } else if (sel == SW_EV_GMAX) {
-                gm = sw_max(gm, sw_g(&c, S.arr[arg][i]));
-            } else if (sel == SW_EV_PACKED) {
-                const int pl = S.arr[arg][i];
-                fa = fa + sw_f(&c, pl, S.nb, S.beta, S.ell);
-                gm = sw_max(gm, sw_g(&c, pl));
-                is += (long long)c.w * (S.arr[SW_A_NB][i] - pl);
-            } else if (sel == SW_EV_P2OK) {
-                is += S.arr[SW_A_PL][i] != S.arr[SW_A_NFIN][i];
-            } else { /* SW_EV_FINAL */
-                const uint64_t m = S.y[arg][i];
-                const int cn = __popcll(m);
-                long long Ssum = 0;
-                for (int t = 0; t < S.T; ++t) {
-                    const uint32_t bit = (uint32_t)((m >> t) & 1ull);
-                    Ssum += bit ? t : 0;
-                    S.plan[(size_t)i * S.T + t] = (uint8_t)bit;
-                }
-                S.planned[i] = cn;
-                fa = fa + sw_f(&c, cn, S.nb, S.beta, S.ell);
-                fb = fb + (cn > 0 ? ((double)Ssum / (double)cn) * S.p[i] : 0.0);
-                gm = sw_max(gm, sw_g(&c, cn));
-                is += cn > 0;
-            }
+            fa = fa + xa[j];
+            fb = fb + xb[j];
         }
         out[lane] = fa;
         out[S.LW + lane] = fb;
     }
-    const uint64_t gw = wave_max(sw_bits(gm));
-    const long long iw = wave_sum(is);
-    if (lane_id() == 0) { sg[wave_id()] = gw; ss[wave_id()] = iw; }
-    __syncthreads();
     if (threadIdx.x == 0) {
-        uint64_t g = 0;
-        long long s = 0;
-        for (int w = 0; w < SW_WAVES; ++w) { g = sg[w] > g ? sg[w] : g; s += ss[w]; }
-        out[2 * S.LW] = sw_from_bits(g);
-        reinterpret_cast<long long*>(out)[2 * S.LW + 1] = s;
+        out[2 * S.LW] = sw_from_bits((uint64_t)S.red[0]);
+        reinterpret_cast<long long*>(out)[2 * S.LW + 1] = S.red[1];
     }
 }
 
 /* ---- placement ---------------------------------------------------------------- */
 
 /* this rank's entries (twin: the k1/k2 of each pack caller) */
-__global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, int src, double Mb,
-                                                   sw_pack_ent* out) {
+__global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const int32_t* src,
+                                                   double Mb, sw_pack_ent* out) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     if (i >= S.P) return;
     sw_pack_ent e;
     e.khi = 0; e.klo = 0; e.st = 0; e.pad = 0;
     if (i < S.NL) {
-        const int n = S.arr[src][i];
+        const int n = src[i];
         if (n > 0) {
             const sw_jobc c = S.jc[i];
             uint64_t k1;
@@ -395,25 +412,48 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, int src
     out[i] = e;
 }
 
-/* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') > key(e)} */
+/* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') >
+ * key(e)}.  Keys are unique (they end in ~job), so the ranks of the active
+ * entries are a permutation of [0, A).  A block ranks kRankPer·kTB entries
+ * against a kRankTile tile held in LDS as 16-B (khi, klo) pairs: one
+ * ds_read_b128 feeds kRankPer compares. */
 constexpr int kRankTile = 1024;
+constexpr int kRankPer = 4;
+struct alignas(16) key2 {
+    uint64_t h, l;
+};
 __global__ __launch_bounds__(kTB) void k_pack_rank(const sw_pack_ent* all, int64_t M, int32_t* rank) {
-    __shared__ uint64_t th[kRankTile], tl[kRankTile];
+    __shared__ key2 tile[kRankTile];
     const int64_t t0 = (int64_t)blockIdx.y * kRankTile;
     for (int x = threadIdx.x; x < kRankTile; x += kTB) {
         const int64_t e = t0 + x;
-        const bool act = e < M && all[e].st != 0;
-        th[x] = act ? all[e].khi : 0;
-        tl[x] = act ? all[e].klo : 0; /* inactive: (0,0) never exceeds an active key */
+        key2 k;
+        k.h = 0; k.l = 0; /* inactive: (0,0) never exceeds an active key */
+        if (e < M && all[e].st != 0) { k.h = all[e].khi; k.l = all[e].klo; }
+        tile[x] = k;
     }
     __syncthreads();
-    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
-    if (e >= M || all[e].st == 0) return;
-    const uint64_t h = all[e].khi, l = all[e].klo;
-    int c = 0;
+    uint64_t h[kRankPer], l[kRankPer];
+    int c[kRankPer];
+    bool act[kRankPer];
+    const int64_t e0 = (int64_t)blockIdx.x * kTB * kRankPer + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kRankPer; ++k) {
+        const int64_t e = e0 + (int64_t)k * kTB;
+        act[k] = e < M && all[e].st != 0;
+        h[k] = act[k] ? all[e].khi : ~0ull;
+        l[k] = act[k] ? all[e].klo : ~0ull;
+        c[k] = 0;
+    }
     const int n = (int)min((int64_t)kRankTile, M - t0);
-    for (int x = 0; x < n; ++x) c += (th[x] > h) || (th[x] == h && tl[x] > l);
-    if (c) atomicAdd(&rank[e], c);
+    for (int x = 0; x < n; ++x) {
+        const key2 v = tile[x];
+#pragma unroll
+        for (int k = 0; k < kRankPer; ++k) c[k] += (v.h > h[k]) || (v.h == h[k] && v.l > l[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kRankPer; ++k)
+        if (act[k] && c[k]) atomicAdd(&rank[e0 + (int64_t)k * kTB], c[k]);
 }
 
 __global__ __launch_bounds__(kTB) void k_pack_scatter(const sw_pack_ent* all, int64_t M,
@@ -426,7 +466,7 @@ __global__ __launch_bounds__(kTB) void k_pack_scatter(const sw_pack_ent* all, in
 template <int E>
 __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
                                                           int64_t M, const int32_t* order,
-                                                          int ydst, int pdst) {
+                                                          uint64_t* ydst, int32_t* pdst) {
     __shared__ sw_xchg X;
     __shared__ sw_pack_lds PL;
     sw_blk blk;
@@ -436,15 +476,18 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
     int act = 0;
     for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
     const int A = blk.sum32(act);
-    for (int i = tid; i < S.NL; i += SW_BLOCK) { S.y[ydst][i] = 0; S.arr[pdst][i] = 0; }
+    for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
     uint32_t st[E];
     uint64_t mk[E];
     int32_t ent[E];
+    const int Am = A > 0 ? A - 1 : 0; /* clamped, unconditional loads: no per-position waits */
+#pragma unroll
+    for (int i = 0; i < E; ++i) ent[i] = order[min(E * tid + i, Am)];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-        const int p = E * tid + i;
-        ent[i] = p < A ? order[p] : -1;
-        st[i] = p < A ? all[ent[i]].st : 0u;
+        const uint32_t v = A > 0 ? all[ent[i]].st : 0u;
+        st[i] = E * tid + i < A ? v : 0u;
+        ent[i] = E * tid + i < A ? ent[i] : -1;
     }
     sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk);
 #pragma unroll
@@ -452,8 +495,8 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
         if (ent[i] < 0) continue;
         const int64_t j = (int64_t)(0xFFFFFFFFu - (uint32_t)(all[ent[i]].klo & 0xFFFFFFFFu));
         if (j >= S.off && j < S.off + S.NL) {
-            S.y[ydst][j - S.off] = mk[i];
-            S.arr[pdst][j - S.off] = (int32_t)(all[ent[i]].st & 0xFFu) - (int32_t)pk_r(st[i]);
+            ydst[j - S.off] = mk[i];
+            pdst[j - S.off] = (int32_t)(all[ent[i]].st & 0xFFu) - (int32_t)pk_r(st[i]);
         }
     }
 }
@@ -476,7 +519,8 @@ struct sw_shard_state {
     double delta = 0.0;
     ShardDev dv;
     /* device */
-    DevBuf<int32_t> w, F, E, l, taken, arr[SW_A_COUNT], planned, prank, porder;
+    DevBuf<int32_t> w, F, E, l, taken, tie, arr[SW_A_COUNT], planned, prank, porder;
+    DevBuf<double> xa;
     DevBuf<double> d, R, p, xsend, xrecv;
     DevBuf<sw_jobc> jc;
     DevBuf<float> keys;
@@ -681,7 +725,8 @@ int op_take(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl) {
 int op_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
-    LAUNCH(S, k_assign, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, rho, (long long)rem,
+    (void)rho; /* k_take stored the tie counts at rho */
+    LAUNCH(S, k_assign, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, (long long)rem,
            (long long)excl);
     return coll_reduce(S, S->red.p, 1, 0, used);
 }
@@ -704,7 +749,11 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
             int64_t* isum) {
     auto* S = (sw_shard_state*)ctx;
     const int64_t LW = S->LW, blk = 2 * LW + 2;
-    LAUNCH(S, k_eval, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, (int)sel, (int)arg, S->xsend.p);
+    SH_TRY(zero_red(S, 2));
+    const int32_t* arr = sel == SW_EV_GMAX || sel == SW_EV_PACKED ? S->arr[arg].p : nullptr;
+    const uint64_t* ys = sel == SW_EV_FINAL ? S->y[arg].p : nullptr;
+    LAUNCH(S, k_eval_jobs, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (int)sel, arr, ys);
+    LAUNCH(S, k_eval_lanes, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, S->xsend.p);
     std::vector<double> all((size_t)blk * S->world);
     SH_TRY(coll_gather(S, S->xsend.p, S->xrecv.p, (size_t)blk * 8, all.data()));
     double g = 0.0;
@@ -743,21 +792,25 @@ int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
     const int64_t M = S->P * S->world;
-    LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, (int)src, Mb, S->psend.p);
+    LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
+           S->psend.p);
     SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr));
     SH_HIP(S, hipMemsetAsync(S->prank.p, 0, (size_t)M * 4, st));
-    dim3 g2(nblk(M), (unsigned)((M + kRankTile - 1) / kRankTile));
+    dim3 g2((unsigned)((M + kTB * kRankPer - 1) / (kTB * kRankPer)),
+            (unsigned)((M + kRankTile - 1) / kRankTile));
     LAUNCH(S, k_pack_rank, g2, dim3(kTB), 0, st, S->pall.p, M, S->prank.p);
     LAUNCH(S, k_pack_scatter, dim3(nblk(M)), dim3(kTB), 0, st, S->pall.p, M, S->prank.p, S->porder.p);
     const ShardDev dv = S->dv;
+    uint64_t* yd = S->y[ydst].p;
+    int32_t* pd = S->arr[pdst].p;
     if (M <= 2 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
     else if (M <= 8 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
     else if (M <= 32 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
     else if (M <= 64 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, (int)ydst, (int)pdst);
+        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
     else
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
     return SW_OK;
@@ -780,7 +833,8 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
     const size_t xbytes = std::max<size_t>({(size_t)(2 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
     bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
                S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
-               S->l.reserve(NL) || S->taken.reserve(NL) || S->plan.reserve(NL * T) ||
+               S->l.reserve(NL) || S->taken.reserve(NL) || S->tie.reserve(NL) ||
+               S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve(kRed) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
                S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
@@ -815,6 +869,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
         v.ell[b] = b < pr->num_bases ? pr->log_bases[b] : 0.0;
     }
     v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->p.p; v.l = S->l.p; v.taken = S->taken.p;
+    v.tie = S->tie.p; v.xa = S->xa.p;
     for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
     for (int a = 0; a < SW_Y_COUNT; ++a) v.y[a] = S->y[a].p;
     v.plan = S->plan.p; v.planned = S->planned.p; v.red = S->red.p;
@@ -842,6 +897,7 @@ void sw_shard_release(sw_handle* h) {
     sw_shard_state* S = h->shard;
     if (S->comm) (void)ncclCommDestroy(S->comm);
     S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
+    S->tie.release(); S->xa.release();
     S->planned.release(); S->prank.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
@@ -852,6 +908,17 @@ void sw_shard_release(sw_handle* h) {
 }
 
 extern "C" {
+
+#ifdef SW_STAMPS
+/* Diagnostic builds only (not part of include/shockwave_amd.h): round-loop
+ * phase cycles accumulated since the last call (which also clears them). */
+int sw_debug_pack_stamps(uint64_t* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sw_pack_stamps), 8 * sizeof(uint64_t)) != hipSuccess)
+        return SW_ERR_HIP;
+    uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sw_pack_stamps), z, sizeof(z)) == hipSuccess ? SW_OK : SW_ERR_HIP;
+}
+#endif
 
 int sw_dist_shard_range(int64_t total_jobs, int32_t world, int32_t rank, int64_t* lo, int64_t* hi) {
     if (!lo || !hi) return SW_ERR_INVALID;

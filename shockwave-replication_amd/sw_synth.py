@@ -28,11 +28,12 @@ except ImportError:  # flat-module use (reference-style sys.path import)
 
 BASES = (0.0, 0.2, 0.4, 0.6, 0.8, 1.0)
 
-# scale_{64,128,256}gpus.json: future_rounds, k, lambda
+# scale_{64,128,256}gpus.json: future_rounds, k, lambda (64: k=10, λ=5;
+# 128: k=1e-3, λ=15; 256: k=1e5, λ=5); 32 GPUs has no JSON and uses 64's
 CLUSTER_CONFIG = {
-    32: dict(T=20, k=1e-3, lam=15.0),
-    64: dict(T=20, k=1e-3, lam=15.0),
-    128: dict(T=20, k=1e1, lam=5.0),
+    32: dict(T=20, k=1e1, lam=5.0),
+    64: dict(T=20, k=1e1, lam=5.0),
+    128: dict(T=20, k=1e-3, lam=15.0),
     256: dict(T=20, k=1e5, lam=5.0),
 }
 
