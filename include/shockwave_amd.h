@@ -217,6 +217,27 @@ typedef struct sw_host_comm {
  * comm->ctx must outlive the handle's solves). */
 int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int32_t world);
 
+/*
+ * Gavel MaxMinFairness allocation for one worker type — the Fig-9 baseline
+ * policy of the Shockwave comparison.  Replaces the ECOS solve of
+ * policies/max_min_fairness.py:68-93 (MaxMinFairnessPolicy →
+ * MaxMinFairnessPolicyWithPerf with unit throughputs, proportional.py:27-44),
+ * which the simulator calls from _compute_allocation (scheduler.py:2386-2466):
+ *
+ *     maximise min_j c_j·x_j   s.t.  Σ_j sf_j·x_j ≤ num_workers,  0 ≤ x_j ≤ 1
+ *
+ * scale_factors[j] = job.scale_factor, coefficients[j] = scale_factor /
+ * priority_weight, in sorted job-id order (policy.py:14-33).  allocation[j]
+ * receives x_j: the unique optimum when capacity binds, otherwise the
+ * analytic centre of the optimal face (the point an interior-point solver
+ * such as ECOS converges to).  level (optional, 2 doubles) receives the
+ * optimal min share t* and the capacity multiplier μ (0 when capacity binds).
+ * Synchronous; num_jobs = 0 is a no-op (policy.flatten returns None).
+ */
+int sw_mmf_allocate(sw_handle* h, int32_t num_jobs, int32_t num_workers,
+                    const int32_t* scale_factors, const double* coefficients, double* allocation,
+                    double* level);
+
 #ifdef __cplusplus
 }
 #endif

@@ -286,3 +286,29 @@ def brute_force_p1(prob: Problem):
         if obj > best[0]:
             best = (obj, x)
     return best
+
+
+class MilpSolver:
+    """ShockwaveScheduler's solver interface (``solve(ProblemArrays) -> dict``)
+    backed by the MILP restatement — the reference's solve path (P1 → P2 →
+    read-back, shockwave.py:330-411) with HiGHS in place of Gurobi.  Used by
+    the simulator-parity tests and tools/sim_parity.py as the oracle run."""
+
+    def __init__(self, rel_gap=1e-3, time_limit=15.0):
+        self.rel_gap = rel_gap
+        self.time_limit = time_limit
+        self.seconds = 0.0
+        self.calls = 0
+
+    def solve(self, arrays):
+        prob = Problem(arrays.w, arrays.d, arrays.F, arrays.E, arrays.R, arrays.p, arrays.T,
+                       arrays.G, arrays.delta, arrays.k, list(arrays.bases))
+        t0 = time.perf_counter()
+        sol = plan_solve(prob, self.rel_gap, self.time_limit)
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        y = sol.y.astype(np.uint8)
+        return {"rc": 0 if sol.p2_status in ("optimal", "no_planned", "time_limit") else 1,
+                "plan": y, "planned_rounds": y.sum(axis=1).astype(np.int32),
+                "objective": sol.objective, "utility": float("nan"), "makespan": float("nan"),
+                "p2_objective": sol.p2_objective, "bound": sol.bound, "iters": 0, "status": 0}

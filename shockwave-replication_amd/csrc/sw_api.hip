@@ -128,6 +128,7 @@ void sw_destroy(sw_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     sw_shard_release(h);
+    sw_mmf_release(h);
     h->d_inst.release(); h->d_w.release(); h->d_F.release(); h->d_E.release();
     h->d_planned.release(); h->d_d.release(); h->d_R.release(); h->d_p.release();
     h->d_plan.release(); h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();

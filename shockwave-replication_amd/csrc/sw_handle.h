@@ -92,8 +92,12 @@ struct sw_handle {
     int32_t runs = 0;
     /* sharded mode (sw_shard.hip) */
     sw_shard_state* shard = nullptr;
+    /* MaxMinFairness allocation buffers (sw_mmf.hip) */
+    void* mmf = nullptr;
 };
 
 /* sw_shard.hip: frees the sharded-mode state and communicator */
 void sw_shard_release(sw_handle* h);
+/* sw_mmf.hip: frees the MaxMinFairness buffers */
+void sw_mmf_release(sw_handle* h);
 

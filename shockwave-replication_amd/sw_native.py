@@ -274,7 +274,7 @@ EXPORTED_SYMBOLS = (
     "sw_plan_solve", "sw_plan_solve_batch", "sw_batch_upload", "sw_batch_run",
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
     "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
-    "sw_dist_init_host",
+    "sw_dist_init_host", "sw_mmf_allocate",
 )
 
 
@@ -334,6 +334,8 @@ def load(path: str | None = None):
     lib.sw_dist_shard_range.restype = C.c_int
     lib.sw_dist_init_host.argtypes = [C.c_void_p, C.POINTER(SwHostComm), C.c_int32, C.c_int32]
     lib.sw_dist_init_host.restype = C.c_int
+    lib.sw_mmf_allocate.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _ip, _dp, _dp, _dp]
+    lib.sw_mmf_allocate.restype = C.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -413,6 +415,21 @@ class Solver:
                     "sw_kernel_times")
         return a.value, b.value, n.value
 
+    # ---- Gavel MaxMinFairness allocation (include/shockwave_amd.h sw_mmf_allocate) ----
+    def mmf_allocate(self, scale_factors, coefficients, num_workers: int):
+        """x_j of the MaxMinFairness LP (one worker type); returns (x, t*, μ)."""
+        sf = np.ascontiguousarray(scale_factors, dtype=np.int32)
+        c = np.ascontiguousarray(coefficients, dtype=np.float64)
+        if len(sf) != len(c):
+            raise ValueError("scale_factors and coefficients must have the same length")
+        x = np.zeros(len(sf), dtype=np.float64)
+        lvl = np.zeros(2, dtype=np.float64)
+        self._check(self.lib.sw_mmf_allocate(self.h, len(sf), int(num_workers),
+                                             sf.ctypes.data_as(_ip), c.ctypes.data_as(_dp),
+                                             x.ctypes.data_as(_dp), lvl.ctypes.data_as(_dp)),
+                    "sw_mmf_allocate")
+        return x, float(lvl[0]), float(lvl[1])
+
     # ---- sharded single instance (include/shockwave_amd.h sw_dist_*) ----
     def dist_init(self, unique_id: bytes, rank: int, world: int):
         """RCCL collectives; unique_id from unique_id() on rank 0, broadcast by the caller."""
@@ -435,6 +452,17 @@ class Solver:
             raise NativeError(f"sw_dist_plan_solve: collective failed: {comm.error!r}")
         self._check(rc, "sw_dist_plan_solve")
         return result_dict(res, local, rc)
+
+
+class MmfAllocator:
+    """The simulator's MaxMinFairness allocation function on the GPU:
+    ``allocator(scale_factors, coefficients, num_workers) -> x``."""
+
+    def __init__(self, device=0, solver=None):
+        self.solver = solver or Solver(device=device)
+
+    def __call__(self, scale_factors, coefficients, num_workers):
+        return self.solver.mmf_allocate(scale_factors, coefficients, num_workers)[0]
 
 
 def unique_id(lib=None) -> bytes:

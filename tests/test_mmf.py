@@ -1,0 +1,72 @@
+"""MaxMinFairness allocation (Gavel baseline, sw_mmf_allocate): the CPU twin
+against the reference LP solved by HiGHS, and the analytic-centre conditions.
+GPU: the HIP kernel against the twin, bit for bit."""
+import numpy as np
+import pytest
+
+import mmf_ref
+
+
+def instances():
+    rng = np.random.default_rng(7)
+    out = []
+    for n, G in [(1, 4), (3, 2), (5, 64), (40, 32), (120, 64), (700, 256), (1500, 256),
+                 (60, 256), (200, 1024), (2, 1)]:
+        sf = rng.choice([1, 2, 4, 8], size=n, p=[0.6, 0.3, 0.09, 0.01]).astype(np.int32)
+        pw = rng.choice([1.0, 1.0, 1.0, 5.0], size=n)
+        out.append((sf, sf / pw, G))
+    sf = np.array([2, 4, 8, 2], dtype=np.int32)  # no unit-width job: t* = 2
+    out.append((sf, sf.astype(float), 64))
+    return out
+
+
+@pytest.mark.parametrize("case", range(len(instances())))
+def test_twin_level_matches_lp(case):
+    sf, c, G = instances()[case]
+    x, t, mu = mmf_ref.twin_allocate(sf, c, G)
+    t_lp, _ = mmf_ref.lp_level(sf, c, G)
+    assert abs(t - t_lp) <= 1e-9 * max(1.0, abs(t_lp))
+    # feasible and optimal: every job gets at least t*, capacity and bounds hold
+    assert np.all(x >= -1e-15) and np.all(x <= 1.0 + 1e-15)
+    assert float(np.dot(sf, x)) <= G * (1 + 1e-12)
+    assert np.min(c * x) >= t * (1 - 1e-12)
+    if mu == 0.0:  # capacity binds: the unique optimum
+        assert np.allclose(x, t / c, rtol=0, atol=1e-15)
+    else:  # analytic centre: stationarity of the barrier on the free jobs
+        free = c > t
+        slack = G - float(np.dot(sf, x))
+        assert abs(mu * slack - 1.0) < 1e-9
+        xf, cf, sff = x[free], c[free], sf[free]
+        h = 1 / xf - 1 / (1 - xf) + cf / (cf * xf - t) - sff * mu
+        scale = 1 / xf + 1 / (1 - xf) + cf / (cf * xf - t)
+        assert np.all(np.abs(h) <= 1e-9 * scale)
+        assert np.all(x[~free] == 1.0)
+
+
+def test_twin_empty_and_deterministic():
+    x, t, mu = mmf_ref.twin_allocate([], [], 8)
+    assert len(x) == 0 and t == 0.0
+    sf, c, G = instances()[5]
+    a = mmf_ref.twin_allocate(sf, c, G)
+    b = mmf_ref.twin_allocate(sf, c, G)
+    assert a[0].tobytes() == b[0].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(instances())))
+def test_gpu_mmf_bit_exact_vs_twin(gpu_solver, case):
+    sf, c, G = instances()[case]
+    xg, tg, mug = gpu_solver.mmf_allocate(sf, c, G)
+    xt, tt, mut = mmf_ref.twin_allocate(sf, c, G)
+    assert xg.tobytes() == xt.tobytes()
+    assert np.float64(tg).tobytes() == np.float64(tt).tobytes()
+    assert np.float64(mug).tobytes() == np.float64(mut).tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_mmf_rejects_bad_input(gpu_solver):
+    import sw_native as sn
+    with pytest.raises(sn.NativeError):
+        gpu_solver.mmf_allocate([1, 0], [1.0, 1.0], 4)
+    with pytest.raises(sn.NativeError):
+        gpu_solver.mmf_allocate([1, 1], [1.0, -1.0], 4)

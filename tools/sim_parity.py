@@ -1,0 +1,84 @@
+"""Simulated Fig-9 metrics with the product solver vs the reference-path oracle.
+
+    python tools/sim_parity.py --trace <name> --gpus 64 --solver {gpu,twin,milp} --out f.json
+
+Runs sw_sim.run_trace for both policies with the chosen Shockwave solver:
+  gpu   the HIP plan kernel + HIP MaxMinFairness kernel (the product; needs a GPU)
+  twin  the bit-exact CPU twins (oracle/plan_twin.c, oracle/mmf_twin.c)
+  milp  the MILP restatement of the reference solve (oracle/milp_ref.py, HiGHS,
+        gap 1e-3, 15 s per MILP as scale_*gpus.json) + the MMF twin
+and writes the metrics as JSON.  The oracle legs are test infrastructure.
+"""
+import argparse
+import contextlib
+import ctypes
+import io
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "shockwave-replication_amd"), os.path.join(ROOT, "oracle")]
+
+import sw_sim  # noqa: E402
+
+
+def twin_solver():
+    import sw_native as sn
+    so = os.path.join(ROOT, "oracle", "_build", "libplan_twin.so")
+    lib = ctypes.CDLL(so)
+    sn.declare_solver_api(lib, "twin_")
+
+    class Twin:
+        def solve(self, arrays):
+            pr, res = arrays.c_problem(), arrays.c_result()
+            rc = lib.twin_plan_solve(ctypes.byref(pr), ctypes.byref(res))
+            if rc < 0:
+                raise ValueError(f"twin rejected the problem ({rc})")
+            return sn.result_dict(res, arrays, rc)
+    return Twin()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", default="220_0.2_5_100_25_4_0,0.5,0.5_0.6,0.3,0.09,0.01_multigpu_dynamic.trace")
+    ap.add_argument("--gpus", type=int, default=64)
+    ap.add_argument("--solver", choices=["gpu", "twin", "milp"], default="gpu")
+    ap.add_argument("--policies", default="shockwave,max_min_fairness")
+    ap.add_argument("--max-jobs", type=int, default=None)
+    ap.add_argument("--time-per-iteration", type=int, default=120)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    cfg_name = f"scale_{max(64, a.gpus)}gpus.json"
+    cfg = json.load(open(os.path.join(ROOT, "data", "configs", cfg_name)))
+    trace = os.path.join(ROOT, "data", "traces", a.trace)
+    if a.solver == "gpu":
+        import sw_native as sn
+        solver = sn.Solver(device=0)
+        mmf = sn.MmfAllocator(solver=solver)
+    else:
+        import mmf_ref
+        mmf = mmf_ref.twin_allocator
+        if a.solver == "twin":
+            solver = twin_solver()
+        else:
+            import milp_ref
+            solver = milp_ref.MilpSolver()
+    out = {"trace": a.trace, "gpus": a.gpus, "solver": a.solver, "config": cfg_name,
+           "time_per_iteration": a.time_per_iteration, "runs": {}}
+    for pol in a.policies.split(","):
+        t0 = time.time()
+        with contextlib.redirect_stdout(io.StringIO()):
+            r = sw_sim.run_trace(pol, trace, a.gpus, a.time_per_iteration, cfg,
+                                 shockwave_solver=solver, mmf_allocator=mmf,
+                                 max_jobs=a.max_jobs)
+        r["wall_s"] = time.time() - t0
+        out["runs"][pol] = r
+        print(pol, json.dumps(r), flush=True)
+    if a.out:
+        json.dump(out, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
