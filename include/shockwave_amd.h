@@ -55,6 +55,10 @@ extern "C" {
 #define SW_STATUS_P1_REPACKED 0x1 /* aggregate P1 counts needed repair to pack */
 #define SW_STATUS_P2_FALLBACK 0x2 /* P2 placement fell back to the P1 plan    */
 #define SW_STATUS_NO_PLANNED 0x4  /* no job has planned rounds (shockwave.py:319-320) */
+/* Which P2 placement was kept: none of these bits = the
+ * density order p_j/(n_j·w_j) placed every round. */
+#define SW_STATUS_P2_WEIGHT_ORDER 0x8 /* the weight order p_j/n_j placed every round   */
+#define SW_STATUS_P2_CLASSWISE 0x10   /* width classes repacked inside the P1 profile  */
 
 /*
  * One plan solve.  Field ↔ reference:

@@ -217,8 +217,10 @@ static int ord_cmp(const void* A, const void* B) {
     return (a->j < b->j) ? -1 : (a->j > b->j);
 }
 
+/* caps: per-round capacity (NULL = G in every round); unit: every width
+ * counts 1 (the class-wise P2 repack, where a class's capacity is in jobs). */
 static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const uint32_t* k2,
-                 uint8_t* y, int32_t* placed) {
+                 uint8_t* y, int32_t* placed, const int32_t* caps, int unit) {
     const int32_t N = P->N, T = P->T, G = P->G;
     size_t NN = N > 0 ? (size_t)N : 1;
     ord_t* ord = (ord_t*)malloc(sizeof(ord_t) * NN);
@@ -229,18 +231,35 @@ static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const 
     for (int32_t j = 0; j < N; ++j)
         if (nin[j] > 0) { ord[A].k1 = k1[j]; ord[A].k2 = k2[j]; ord[A].j = j; ++A; }
     qsort(ord, (size_t)A, sizeof(ord_t), ord_cmp);
-    for (int32_t i = 0; i < A; ++i) { r[i] = nin[ord[i].j]; ww[i] = P->jc[ord[i].j].w; }
+    for (int32_t i = 0; i < A; ++i) { r[i] = nin[ord[i].j]; ww[i] = unit ? 1 : P->jc[ord[i].j].w; }
     memset(y, 0, NN * (size_t)T);
     int64_t H[SW_TMAX + 1], SH[SW_TMAX + 1], need[SW_TMAX];
+    int64_t Lsum[SW_TMAX + 1];
+    int32_t fut[SW_TMAX];
     for (int32_t t = 0; t < T; ++t) {
         int32_t R = T - t;
-        int64_t cap = G;
+        int64_t cap = caps ? caps[t] : G;
         for (int32_t v = 0; v <= R; ++v) { H[v] = 0; SH[v] = 0; }
         for (int32_t i = 0; i < A; ++i) H[r[i] < R ? r[i] : R] += ww[i];
+        /* Lsum[x] = the x smallest capacities of the rounds after t: the room
+         * jobs with more than m rounds left have after this round is
+         * Lsum[R−1−m] (= G·(R−1−m) for uniform capacity) */
+        Lsum[0] = 0;
+        if (caps) {
+            for (int32_t u = 0; u < R - 1; ++u) fut[u] = caps[t + 1 + u];
+            for (int32_t u = 1; u < R - 1; ++u) { /* insertion sort, ascending */
+                int32_t v = fut[u], x = u - 1;
+                while (x >= 0 && fut[x] > v) { fut[x + 1] = fut[x]; --x; }
+                fut[x + 1] = v;
+            }
+            for (int32_t u = 0; u < R - 1; ++u) Lsum[u + 1] = Lsum[u] + fut[u];
+        } else {
+            for (int32_t u = 0; u < R - 1; ++u) Lsum[u + 1] = Lsum[u] + G;
+        }
         for (int32_t m = 0; m < R; ++m) {
             int64_t D = 0;
             for (int32_t v = m + 1; v <= R; ++v) D += H[v] * (int64_t)(v - m);
-            need[m] = D - (int64_t)G * (R - 1 - m);
+            need[m] = D - Lsum[R - 1 - m];
         }
         memset(sel, 0, (size_t)(A > 0 ? A : 1));
         /* tiers: jobs with more than m rounds left must shed enough now */
@@ -288,15 +307,21 @@ static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const 
 
 /* The packer over plain arrays, for the sharded CPU engine (oracle/shard_twin.c):
  * pack() reads only N, T, G and the widths. */
-void twin_pack_arrays(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
-                      const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed) {
+void twin_pack_arrays_caps(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
+                           const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed,
+                           const int32_t* caps, int unit) {
     twin_t P;
     memset(&P, 0, sizeof(P));
     P.N = N; P.T = T; P.G = G;
     P.jc = (sw_jobc*)calloc(N > 0 ? (size_t)N : 1, sizeof(sw_jobc));
     for (int32_t j = 0; j < N; ++j) P.jc[j].w = w[j];
-    pack(&P, nin, k1, k2, y, placed);
+    pack(&P, nin, k1, k2, y, placed, caps, unit);
     free(P.jc);
+}
+
+void twin_pack_arrays(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
+                      const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed) {
+    twin_pack_arrays_caps(N, T, G, w, nin, k1, k2, y, placed, NULL, 0);
 }
 
 static void build(twin_t* P, const sw_problem* pr) {
@@ -424,7 +449,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
                     k1[j] = 0; k2[j] = 0;
                 }
             }
-            pack(&P, nb, k1, k2, ord ? y2 : y1, ord ? placed2 : placed);
+            pack(&P, nb, k1, k2, ord ? y2 : y1, ord ? placed2 : placed, NULL, 0);
             int64_t dfc = 0;
             double Mp = 0.0;
             const int32_t* pl = ord ? placed2 : placed;
@@ -456,14 +481,62 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     }
     memcpy(nb, nbest, sizeof(int32_t) * NN);
     memcpy(y1, ybest, NN * (size_t)T); /* y1 = best P1 plan */
-    /* ---- P2: priority placement of the same counts (shockwave.py:281-328) ---- */
-    for (int32_t j = 0; j < N; ++j) {
-        k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] / (double)nb[j]) : 0;
-        k2[j] = 0;
+    /* ---- P2: priority placement of the same counts (shockwave.py:281-328).
+     * Σ_t t·y_jt is weighted by p_j/n_j per job while a job occupies w_j
+     * GPUs, so the placements tried, first success kept, are
+     *   (a) density order p_j/(n_j·w_j);
+     *   (b) the weight order p_j/n_j;
+     *   (c) class-wise: each width class, in ascending width, repacked with
+     *       unit widths and order p_j/n_j inside the per-round capacity that
+     *       class has in the P1 placement y1 (exact for unit widths, so it
+     *       places every round);
+     * and the P1 placement if none does (shockwave.py:325-326). ---- */
+    int ok2 = 0;
+    for (int att = 0; att < 2 && !ok2; ++att) {
+        for (int32_t j = 0; j < N; ++j) {
+            k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] /
+                                        (double)(att == 0 ? nb[j] * P.jc[j].w : nb[j]))
+                              : 0;
+            k2[j] = 0;
+        }
+        pack(&P, nb, k1, k2, y2, placed, NULL, 0);
+        ok2 = 1;
+        for (int32_t j = 0; j < N; ++j) ok2 &= (placed[j] == nb[j]);
+        if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
     }
-    pack(&P, nb, k1, k2, y2, placed);
-    int ok2 = 1;
-    for (int32_t j = 0; j < N; ++j) ok2 &= (placed[j] == nb[j]);
+    if (!ok2) {
+        int32_t caps[SW_TMAX];
+        int32_t* nc = placed2; /* class counts: nb on the class, 0 elsewhere */
+        uint8_t* yc = (uint8_t*)malloc(NN * T);
+        memset(y2, 0, NN * (size_t)T);
+        ok2 = 1;
+        int32_t wprev = 0;
+        while (1) {
+            int32_t wc = 0x7FFFFFFF;
+            for (int32_t j = 0; j < N; ++j)
+                if (nb[j] > 0 && P.jc[j].w > wprev && P.jc[j].w < wc) wc = P.jc[j].w;
+            if (wc == 0x7FFFFFFF) break;
+            for (int32_t t = 0; t < T; ++t) caps[t] = 0;
+            for (int32_t j = 0; j < N; ++j) {
+                int cls = nb[j] > 0 && P.jc[j].w == wc;
+                nc[j] = cls ? nb[j] : 0;
+                k1[j] = cls ? sw_bits(pr->priority[j] / (double)nb[j]) : 0;
+                k2[j] = 0;
+                if (cls)
+                    for (int32_t t = 0; t < T; ++t) caps[t] += y1[(size_t)j * T + t];
+            }
+            pack(&P, nc, k1, k2, yc, placed, caps, 1);
+            for (int32_t j = 0; j < N; ++j) {
+                if (nc[j] > 0) {
+                    ok2 &= (placed[j] == nc[j]);
+                    memcpy(y2 + (size_t)j * T, yc + (size_t)j * T, (size_t)T);
+                }
+            }
+            wprev = wc;
+        }
+        free(yc);
+        if (ok2) status |= SW_STATUS_P2_CLASSWISE;
+    }
     uint8_t* yf = y2;
     if (!ok2) { yf = y1; status |= SW_STATUS_P2_FALLBACK; }
     free(k1); free(k2); free(nbest);

@@ -25,8 +25,9 @@
 #include "../shockwave-replication_amd/csrc/sw_shard_ctl.h"
 #include "../shockwave-replication_amd/csrc/sw_validate.h"
 
-void twin_pack_arrays(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
-                      const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed);
+void twin_pack_arrays_caps(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
+                           const uint64_t* k1, const uint32_t* k2, uint8_t* y, int32_t* placed,
+                           const int32_t* caps, int unit);
 
 typedef struct {
     const sw_host_comm* comm;
@@ -296,8 +297,10 @@ typedef struct {
     int32_t nin;
 } pk_t;
 
-static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
-    eng_t* E = (eng_t*)ctx;
+/* mode 1/3/2/4 = sw_shard_ops.pack; mode 5 = pack_class (jobs of width wc,
+ * unit widths, per-round capacities caps, other jobs untouched) */
+static int e_pack_any(eng_t* E, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
+                      int32_t wc, const int32_t* caps) {
     const int64_t P = E->P > 0 ? E->P : 1, N = E->N;
     pk_t* mine = (pk_t*)calloc((size_t)P, sizeof(pk_t));
     pk_t* all = (pk_t*)calloc((size_t)P * E->world, sizeof(pk_t));
@@ -309,10 +312,13 @@ static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst,
     int rc = -1;
     if (!mine || !all || !nin || !k1 || !k2 || !placed || !y) goto out;
     for (int32_t i = 0; i < E->NL; ++i) {
-        const int32_t n = E->arr[src][i];
+        const int32_t n = (mode == 5 && E->jc[i].w != wc) ? 0 : E->arr[src][i];
         mine[i].nin = n;
         if (n > 0) {
-            if (mode != 2) {
+            if (mode == 4) {
+                mine[i].k1 = sw_bits(E->p[i] / (double)(n * E->jc[i].w));
+                mine[i].k2 = 0;
+            } else if (mode != 2 && mode != 5) {
                 const double lvl = sw_g(&E->jc[i], n - 1);
                 const int crit = E->k > 0.0 && lvl > Mb;
                 mine[i].k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)E->jc[i].w : 0);
@@ -330,9 +336,11 @@ static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst,
         k1[j] = all[j].k1;
         k2[j] = all[j].k2;
     }
-    twin_pack_arrays((int32_t)N, E->T, E->G, E->w_all, nin, k1, k2, y, placed);
+    twin_pack_arrays_caps((int32_t)N, E->T, E->G, E->w_all, nin, k1, k2, y, placed,
+                          mode == 5 ? caps : NULL, mode == 5);
     for (int32_t i = 0; i < E->NL; ++i) {
         const int64_t j = E->off + i;
+        if (mode == 5 && !(E->jc[i].w == wc && E->arr[src][i] > 0)) continue;
         uint64_t m = 0;
         for (int32_t t = 0; t < E->T; ++t) m |= (uint64_t)y[(size_t)j * E->T + t] << t;
         E->y[ydst][i] = m;
@@ -341,6 +349,39 @@ static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst,
 out:
     free(mine); free(all); free(nin); free(k1); free(k2); free(placed); free(y);
     return rc;
+}
+
+static int e_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
+    return e_pack_any((eng_t*)ctx, mode, src, Mb, ydst, pdst, 0, NULL);
+}
+
+static int e_pack_class(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
+                        int32_t pdst) {
+    return e_pack_any((eng_t*)ctx, 5, src, 0.0, ydst, pdst, wc, caps);
+}
+
+static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps,
+                        int32_t* next_w) {
+    eng_t* E = (eng_t*)ctx;
+    int64_t buf[SW_TMAX];
+    uint64_t nx = 0; /* max of ~next: the min width above wc */
+    for (int32_t t = 0; t < E->T; ++t) buf[t] = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        if (E->arr[src][i] <= 0) continue;
+        const int32_t w = E->jc[i].w;
+        if (w == wc)
+            for (int32_t t = 0; t < E->T; ++t) buf[t] += (int64_t)((E->y[ysrc][i] >> t) & 1u);
+        if (w > wc) {
+            const uint64_t v = 0xFFFFFFFFull - (uint64_t)w;
+            nx = v > nx ? v : nx;
+        }
+    }
+    int rc = E->comm->allreduce_sum_i64(E->comm->ctx, buf, E->T);
+    if (!rc) rc = E->comm->allreduce_max_u64(E->comm->ctx, &nx, 1);
+    if (rc) return -1;
+    for (int32_t t = 0; t < E->T; ++t) caps[t] = (int32_t)buf[t];
+    *next_w = nx == 0 ? 0x7FFFFFFF : (int32_t)(0xFFFFFFFFull - nx);
+    return 0;
 }
 
 /*
@@ -406,6 +447,8 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.copy = e_copy;
     ops.copy_y = e_copy_y;
     ops.pack = e_pack;
+    ops.class_caps = e_class_caps;
+    ops.pack_class = e_pack_class;
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,
                             &res->status);

@@ -98,8 +98,19 @@ typedef struct sw_shard_ops {
     int (*copy)(void* ctx, int32_t dst, int32_t src);   /* count arrays */
     int (*copy_y)(void* ctx, int32_t dst, int32_t src); /* bitmask arrays */
     /* place arr[src] rounds per job (twin: pack); mode 1/3 = P1 orders A/B
-     * (Mb = makespan of arr[src]), 2 = P2 order p/n.  Writes Y[ydst], arr[pdst] */
+     * (Mb = makespan of arr[src]), 2 = P2 weight order p/n, 4 = P2 density
+     * order p/(n·w).  Writes Y[ydst], arr[pdst] */
     int (*pack)(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst);
+    /* class-wise P2 (twin: the (c) placement).  caps[t] = #{j : arr[src]_j > 0,
+     * w_j = wc, bit t of Y[ysrc]_j} summed over all ranks; next_w = the
+     * smallest width > wc among jobs with arr[src]_j > 0 (0x7FFFFFFF if none) */
+    int (*class_caps)(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps,
+                      int32_t* next_w);
+    /* pack the jobs of width wc (arr[src] rounds, order p/n, unit widths) into
+     * per-round capacities caps; writes their rows of Y[ydst] and arr[pdst]
+     * and leaves every other job untouched */
+    int (*pack_class)(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
+                      int32_t pdst);
 } sw_shard_ops;
 
 /* Job range of `rank` (sw_dist_shard_range in include/shockwave_amd.h). */
@@ -355,13 +366,36 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             status |= SW_STATUS_P1_REPACKED;
             c->C -= deficit;
         }
-        /* P2: priority placement of the best packed counts (shockwave.py:281-328) */
-        SWC_RUN(o->pack(o->ctx, 2, SW_A_NFIN, 0.0, SW_Y_2, SW_A_PL));
-        c->steps++;
+        /* P2: priority placement of the best packed counts (shockwave.py:281-328);
+         * (a) density order, (b) weight order, (c) class-wise inside the P1
+         * profile — first that places every round (twin: the P2 block) */
+        int ok2 = 0;
         int64_t bad;
-        SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
-        c->steps++;
-        const int ok2 = bad == 0;
+        for (int att = 0; att < 2 && !ok2; ++att) {
+            SWC_RUN(o->pack(o->ctx, att == 0 ? 4 : 2, SW_A_NFIN, 0.0, SW_Y_2, SW_A_PL));
+            c->steps++;
+            SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
+            c->steps++;
+            ok2 = bad == 0;
+            if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
+        }
+        if (!ok2) {
+            int32_t caps[SW_TMAX];
+            int32_t wc = 0, next_w = 0;
+            SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, 0, caps, &next_w));
+            c->steps++;
+            while (next_w != 0x7FFFFFFF) {
+                wc = next_w;
+                SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, wc, caps, &next_w));
+                c->steps++;
+                SWC_RUN(o->pack_class(o->ctx, SW_A_NFIN, wc, caps, SW_Y_2, SW_A_PL));
+                c->steps++;
+            }
+            SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
+            c->steps++;
+            ok2 = bad == 0;
+            if (ok2) status |= SW_STATUS_P2_CLASSWISE;
+        }
         if (!ok2) status |= SW_STATUS_P2_FALLBACK;
         int64_t any;
         SWC_RUN(o->eval(o->ctx, SW_EV_FINAL, ok2 ? SW_Y_2 : SW_Y_BEST, c->lanesA, c->lanesB, &gm,
