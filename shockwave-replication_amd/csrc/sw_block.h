@@ -130,6 +130,22 @@ __device__ __forceinline__ T wave_sufscan(T v) {
     return v;
 }
 
+/* Ascending bitonic sort of one int32 per lane across the wave. */
+__device__ __forceinline__ int32_t wave_sort_asc_i32(int32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int32_t o = __shfl_xor(v, j, 64);
+            const bool up = (lane & k) == 0;
+            const bool lower = (lane & j) == 0;
+            v = (lower == up) ? min(v, o) : max(v, o);
+        }
+    }
+    return v;
+}
+
 /* Fixed halving tree over the wave (p[i] += p[i+h], h = 32 … 1); the result
  * is valid in lane 0. */
 __device__ __forceinline__ double wave_dettree(double x) {

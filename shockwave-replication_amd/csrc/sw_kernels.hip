@@ -88,6 +88,9 @@ struct Ctx {
     uint64_t* sbuf; /* ONE: [2][2][1024] bitonic exchange; else [2][NP] keys */
     int32_t *H, *SH;
     sw_pack_lds* PL;
+    /* class-wise P2 (MODE 5): the class width and its per-round capacity (LDS) */
+    int32_t pwc;
+    int32_t* caps;
     int64_t* misc;
     /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
     sw_jobc jcs[SW_JPT];
@@ -534,15 +537,28 @@ struct Ctx {
     }
 
     /* Order key of job j for pack<MODE> (twin: the k1/k2 of each caller). */
+    /* rounds job j brings to pack<MODE>: MODE 5 keeps only the class pwc */
+    __device__ __forceinline__ int nin_of(int MODE, const uint8_t* nin, int j) const {
+        return (MODE == 5 && w_in[j] != pwc) ? 0 : (int)nin[j];
+    }
+    /* does pack<MODE> own job j's row (MODE 5: only its class) */
+    __device__ __forceinline__ bool owns(int MODE, const uint8_t* nin, int j) const {
+        return MODE != 5 || (w_in[j] == pwc && nin[j] > 0);
+    }
+
+    /* Order key of job j for pack<MODE> (twin: the k1/k2 of each caller). */
     __device__ __forceinline__ void key_of(int MODE, const uint8_t* nin, double Mb, int j, int s,
                                            uint64_t& khi, uint64_t& klo) const {
-        const int nj = nin[j];
+        const int nj = nin_of(MODE, nin, j);
         khi = 0;
         klo = 0;
         if (nj > 0) {
             uint64_t k1;
             uint32_t k2;
-            if (MODE != 2) {
+            if (MODE == 4) {
+                k1 = sw_bits(p_in[j] / (double)(nj * jc(j, s).w));
+                k2 = 0;
+            } else if (MODE != 2 && MODE != 5) {
                 const double lvl = gval(j, s, nj - 1);
                 const bool crit = k > 0.0 && lvl > Mb;
                 k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (MODE == 3 ? (uint64_t)jc(j, s).w : 0);
@@ -558,14 +574,18 @@ struct Ctx {
 
     /*
      * twin: pack — place nin[j] rounds per job into T rounds of capacity G.
-     * MODE 1 / 3: P1 packing orders A / B; MODE 2: P2 order (p_j / n_j).
+     * MODE 1 / 3: P1 packing orders A / B; MODE 2: P2 weight order p_j/n_j;
+     * MODE 4: P2 density order p_j/(n_j·w_j); MODE 5: class-wise P2 — the jobs
+     * of width pwc with unit widths inside the per-round capacities caps[t],
+     * every other job's row and count untouched.
      * Writes y[job] (round bitmask) and placed_out[job].
      */
     __device__ __forceinline__ void pack(int MODE, const uint8_t* nin, uint64_t* y,
                                          uint8_t* placed_out) {
         __syncthreads();
         double Mb = 0.0;
-        if (MODE != 2) {
+        const int32_t* capsp = MODE == 5 ? caps : nullptr;
+        if (MODE == 1 || MODE == 3) {
             for_jobs([&](int j, int s) { Mb = sw_max(Mb, gval(j, s, nin[j])); });
             Mb = blk.dmax(Mb);
         }
@@ -577,8 +597,8 @@ struct Ctx {
             for (int s = 0; s < E; ++s) { khi[s] = 0; klo[s] = 0; }
             for_jobs([&](int j, int s) {
                 key_of(MODE, nin, Mb, j, s, khi[s], klo[s]);
-                act_l += nin[j] > 0;
-                y[j] = 0;
+                act_l += nin_of(MODE, nin, j) > 0;
+                if (owns(MODE, nin, j)) y[j] = 0;
             });
             const int A_ = (int)blk.sum(act_l);
             sort_regs(khi, klo);
@@ -590,10 +610,14 @@ struct Ctx {
                 const int p = E * (int)threadIdx.x + s;
                 mk[s] = 0;
                 jp[s] = (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
-                st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | ((uint32_t)w_in[jp[s]] << 8)) : 0u;
+                const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
+                st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
             }
-            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk);
-            for_jobs([&](int j, int s) { (void)s; placed_out[j] = 0; });
+            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp);
+            for_jobs([&](int j, int s) {
+                (void)s;
+                if (owns(MODE, nin, j)) placed_out[j] = 0;
+            });
             __syncthreads();
 #pragma unroll
             for (int s = 0; s < E; ++s) {
@@ -616,8 +640,8 @@ struct Ctx {
                 key_of(MODE, nin, Mb, j, 0, khi, klo);
                 shi[j] = khi;
                 slo[j] = klo;
-                act_l += nin[j] > 0;
-                y[j] = 0;
+                act_l += nin_of(MODE, nin, j) > 0;
+                if (owns(MODE, nin, j)) y[j] = 0;
             }
             const int A_ = (int)blk.sum(act_l);
             sort_global(NPg);
@@ -626,13 +650,14 @@ struct Ctx {
                 const int j = (int)(0xFFFFFFFFu - (uint32_t)(slo[p] & 0xFFFFFFFFu));
                 const int s = tslot(p, PPL);
                 pord[s] = j;
-                pst[s] = (uint32_t)nin[j] | ((uint32_t)w_in[j] << 8);
+                pst[s] = (uint32_t)nin[j] | ((MODE == 5 ? 1u : (uint32_t)w_in[j]) << 8);
                 pmask[s] = 0;
             }
             __syncthreads();
-            if (wave_id() == 0) rounds(A_, PPL);
+            if (wave_id() == 0) rounds(A_, PPL, capsp);
             __syncthreads();
-            for (int j = jlo(); j < jhi(); ++j) placed_out[j] = 0;
+            for (int j = jlo(); j < jhi(); ++j)
+                if (owns(MODE, nin, j)) placed_out[j] = 0;
             __syncthreads();
             for (int p = threadIdx.x; p < A_; p += SW_BLOCK) {
                 const int s = tslot(p, PPL);
@@ -647,12 +672,12 @@ struct Ctx {
     /* The round loop of pack, run by wave 0 alone (twin: the t loop of
      * pack).  Lane L owns positions [L·PPL, L·PPL + PPL) (prefix order =
      * lane-major); their state lives at tslot(p). */
-    __device__ __forceinline__ void rounds(int A_, int PPL) {
-        rounds_mem(A_, PPL);
+    __device__ __forceinline__ void rounds(int A_, int PPL, const int32_t* capsp) {
+        rounds_mem(A_, PPL, capsp);
     }
 
     /* !ONE: the same loop over position state in the HBM workspace. */
-    __device__ __forceinline__ void rounds_mem(int A_, int PPL) {
+    __device__ __forceinline__ void rounds_mem(int A_, int PPL, const int32_t* capsp) {
         const int lane = lane_id();
         /* lane owns positions p = lane·PPL + i, i < cnt; slot(p) = i·64 + lane */
         const int p0 = lane * PPL;
@@ -660,7 +685,7 @@ struct Ctx {
         const int my = cnt_l > 0 ? cnt_l : 0;
         for (int t = 0; t < T; ++t) {
             const int R = T - t;
-            int64_t cap = G;
+            int64_t cap = capsp ? capsp[t] : G;
             H[lane] = 0;
             SH[lane] = 0;
             if (lane == 0) { H[64] = 0; SH[64] = 0; }
@@ -671,13 +696,12 @@ struct Ctx {
                 atomicAdd(&H[rr], (int32_t)st_w(s));
             }
             wave_sync();
-            /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m); lane m holds m */
+            /* need_m = Σ_{v>m} (v−m)·H[v] − room_m; lane m holds m */
             const int64_t hv = (lane + 1 <= R) ? (int64_t)H[lane + 1] : 0;
             const int64_t S0 = wave_sufscan(hv);
             const int64_t S1 = wave_sufscan(hv * (int64_t)(lane + 1));
-            const int64_t need = (lane < R)
-                                     ? (S1 - (int64_t)lane * S0) - (int64_t)G * (R - 1 - lane)
-                                     : (int64_t)-1;
+            const int64_t room = (int64_t)sw_pack_room(capsp, t, R, G);
+            const int64_t need = (lane < R) ? (S1 - (int64_t)lane * S0) - room : (int64_t)-1;
             /* tiers, highest m first */
             int mstart = R - 1;
             while (mstart >= 0) {
@@ -798,6 +822,8 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.PL = (sw_pack_lds*)carve(sizeof(sw_pack_lds));
     c.H = c.PL->H[0];
     c.SH = c.PL->SH[0];
+    c.caps = c.PL->H[1]; /* spare row of the pack LDS */
+    c.pwc = 0;
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
     if (threadIdx.x < SW_BMAX) {
         bt[threadIdx.x] = I->beta[threadIdx.x];
@@ -876,17 +902,10 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             SW_STAMP(1);
             mode = 1;
         }
+        if (mode == 2) break; /* P2 below */
         uint8_t* pl = (mode == 3) ? c.placed2 : c.placed;
-        const uint8_t* nin = (mode == 2) ? c.nfin : c.nbest;
         uint64_t* yd = (mode == 1) ? c.ycur : c.y2;
-        c.pack(mode, nin, yd, pl);
-        if (mode == 2) {
-            SW_STAMP(4);
-            int64_t bad_l = 0;
-            c.for_jobs([&](int j, int s) { (void)s; bad_l += (c.placed[j] != c.nfin[j]); });
-            ok2 = c.blk.sum(bad_l) == 0;
-            break;
-        }
+        c.pack(mode, c.nbest, yd, pl);
         int64_t def_l = 0;
         double fs = 0.0, gm = 0.0;
         c.for_jobs([&](int j, int s) {
@@ -932,6 +951,48 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         }
         __syncthreads();
     }
+    /* ---- P2 (twin: the P2 block): (a) density order, (b) weight order,
+     *      (c) class-wise inside the P1 profile — first that places every
+     *      round, else the P1 placement ---- */
+    auto p2_ok = [&]() {
+        int64_t bad_l = 0;
+        c.for_jobs([&](int j, int s) { (void)s; bad_l += (c.placed[j] != c.nfin[j]); });
+        return c.blk.sum(bad_l) == 0;
+    };
+    ok2 = false;
+    for (int att = 0; att < 2 && !ok2; ++att) {
+        c.pack(att == 0 ? 4 : 2, c.nfin, c.y2, c.placed);
+        ok2 = p2_ok();
+        if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
+    }
+    if (!ok2) {
+        int32_t wprev = 0;
+        while (true) {
+            int32_t wl = 0x7FFFFFFF;
+            c.for_jobs([&](int j, int s) {
+                const int32_t w = c.jc(j, s).w;
+                if (c.nfin[j] > 0 && w > wprev && w < wl) wl = w;
+            });
+            const int32_t wc = c.blk.min32(wl);
+            if (wc == 0x7FFFFFFF) break;
+            __syncthreads(); /* the previous class's pack has read caps */
+            if (threadIdx.x < 64) c.caps[threadIdx.x] = 0;
+            __syncthreads();
+            c.for_jobs([&](int j, int s) {
+                if (c.nfin[j] > 0 && c.jc(j, s).w == wc) {
+                    const uint64_t m = c.ybest[j];
+                    for (int t = 0; t < c.T; ++t)
+                        if ((m >> t) & 1ull) atomicAdd(&c.caps[t], 1);
+                }
+            });
+            c.pwc = wc;
+            c.pack(5, c.nfin, c.y2, c.placed);
+            wprev = wc;
+        }
+        ok2 = p2_ok();
+        if (ok2) status |= SW_STATUS_P2_CLASSWISE;
+    }
+    SW_STAMP(4);
     if (!ok2) status |= SW_STATUS_P2_FALLBACK;
 
     /* ---- emit ---- */

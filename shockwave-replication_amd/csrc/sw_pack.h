@@ -68,9 +68,27 @@ struct sw_pack_lds {
  * E up to 32 positions per thread, per-position branches each held a 64-bit
  * exec mask and spilled the SGPR file.
  */
+/* Room after round t for jobs with more than m rounds left, lane m:
+ * the R−1−m smallest capacities of rounds t+1 … T−1 (twin: Lsum[R−1−m]);
+ * G·(R−1−m) when every round has capacity G (caps == nullptr). */
+__device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int R, int G) {
+    const int lane = lane_id();
+    if (!caps) return G * (R - 1 - lane);
+    int32_t v = (lane < R - 1) ? caps[t + 1 + lane] : 0x7FFFFFFF;
+    v = wave_sort_asc_i32(v);
+    v = (lane < R - 1) ? v : 0;
+    const int32_t ps = wave_incscan_i32(v);
+    const int x = R - 1 - lane;
+    const int32_t pv = __shfl(ps, x > 0 ? x - 1 : 0, 64);
+    return x > 0 ? pv : 0;
+}
+
+/* caps: per-round capacity in LDS (nullptr = G every round) — the class-wise
+ * P2 repack, where positions carry unit widths */
 template <int E>
 __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int A, int T, int G,
-                                               uint32_t (&st)[E], uint64_t (&mk)[E]) {
+                                               uint32_t (&st)[E], uint64_t (&mk)[E],
+                                               const int32_t* caps = nullptr) {
     const int tid = threadIdx.x;
     const int lane = lane_id();
 #ifdef SW_STAMPS
@@ -89,7 +107,7 @@ __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int 
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
-        int32_t cap = G;
+        int32_t cap = caps ? caps[t] : G;
         __syncthreads(); /* Hu holds the placements of round t − 1 */
         /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
          * lane m holds hv = H[m + 1] */
@@ -99,7 +117,8 @@ __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int 
         /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-        const int32_t need = (lane < R) ? (S1 - lane * S0) - G * (R - 1 - lane) : -1;
+        const int32_t room = sw_pack_room(caps, t, R, G);
+        const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
         SWP_STAMP(1);
         /* tiers: jobs with more than m rounds left must shed enough now */
         int mstart = R - 1;

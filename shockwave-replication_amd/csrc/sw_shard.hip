@@ -383,19 +383,24 @@ __global__ __launch_bounds__(SW_BLOCK) void k_eval_lanes(ShardDev S, double* out
 /* ---- placement ---------------------------------------------------------------- */
 
 /* this rank's entries (twin: the k1/k2 of each pack caller) */
+/* mode 1/3 P1 orders A/B, 2 P2 weight order, 4 P2 density order, 5 the
+ * class-wise P2 repack of width wc (unit widths) */
 __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const int32_t* src,
-                                                   double Mb, sw_pack_ent* out) {
+                                                   double Mb, int wc, sw_pack_ent* out) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     if (i >= S.P) return;
     sw_pack_ent e;
     e.khi = 0; e.klo = 0; e.st = 0; e.pad = 0;
     if (i < S.NL) {
-        const int n = src[i];
+        const sw_jobc c = S.jc[i];
+        const int n = (mode == 5 && c.w != wc) ? 0 : src[i];
         if (n > 0) {
-            const sw_jobc c = S.jc[i];
             uint64_t k1;
             uint32_t k2;
-            if (mode != 2) {
+            if (mode == 4) {
+                k1 = sw_bits(S.p[i] / (double)(n * c.w));
+                k2 = 0;
+            } else if (mode != 2 && mode != 5) {
                 const double lvl = sw_g(&c, n - 1);
                 const bool crit = S.k > 0.0 && lvl > Mb;
                 k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)c.w : 0);
@@ -406,10 +411,25 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
             }
             e.khi = k1;
             e.klo = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(S.off + i));
-            e.st = (uint32_t)n | ((uint32_t)c.w << 8);
+            e.st = (uint32_t)n | ((mode == 5 ? 1u : (uint32_t)c.w) << 8);
         }
     }
     out[i] = e;
+}
+
+/* class-wise P2: red[t] = #{local j : src_j > 0, w_j = wc, bit t of ys_j};
+ * red[64] = max over local j with src_j > 0 and w_j > wc of ~w_j */
+__global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* src,
+                                                    const uint64_t* ys, int wc) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t m = 0, nx = 0;
+    if (i < S.NL && src[i] > 0) {
+        const int w = S.jc[i].w;
+        if (w == wc) m = ys[i];
+        if (w > wc) nx = 0xFFFFFFFFull - (uint64_t)w;
+    }
+    for (int t = 0; t < S.T; ++t) red_add(S.red + t, (long long)((m >> t) & 1ull));
+    red_umax(S.red + 64, nx);
 }
 
 /* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') >
@@ -463,20 +483,26 @@ __global__ __launch_bounds__(kTB) void k_pack_scatter(const sw_pack_ent* all, in
 }
 
 /* the round loop over the global order; writes this rank's rows */
+/* capsd: per-round capacities of the class-wise repack (nullptr = G); then
+ * only the entries' rows are written, every other job is left untouched */
 template <int E>
 __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
                                                           int64_t M, const int32_t* order,
-                                                          uint64_t* ydst, int32_t* pdst) {
+                                                          uint64_t* ydst, int32_t* pdst,
+                                                          const int32_t* capsd) {
     __shared__ sw_xchg X;
     __shared__ sw_pack_lds PL;
+    __shared__ int32_t capsL[64];
     sw_blk blk;
     blk.X = &X;
     blk.par = 0;
     const int tid = threadIdx.x;
+    if (capsd && tid < S.T) capsL[tid] = capsd[tid];
     int act = 0;
     for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
-    const int A = blk.sum32(act);
-    for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
+    const int A = blk.sum32(act); /* its barrier publishes capsL */
+    if (!capsd)
+        for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
     uint32_t st[E];
     uint64_t mk[E];
     int32_t ent[E];
@@ -489,7 +515,7 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
         st[i] = E * tid + i < A ? v : 0u;
         ent[i] = E * tid + i < A ? ent[i] : -1;
     }
-    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk);
+    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr);
 #pragma unroll
     for (int i = 0; i < E; ++i) {
         if (ent[i] < 0) continue;
@@ -528,8 +554,10 @@ struct sw_shard_state {
     DevBuf<uint8_t> plan;
     DevBuf<long long> red;
     DevBuf<sw_pack_ent> psend, pall;
+    DevBuf<int32_t> caps; /* class-wise P2 capacities */
     /* pinned staging */
     HostBuf<uint8_t> hx;
+    HostBuf<int32_t> hcaps;
     std::vector<int32_t> w_all;
     std::vector<uint8_t> hgather;
 };
@@ -788,12 +816,18 @@ int op_copy_y(void* ctx, int32_t dst, int32_t src) {
     return SW_OK;
 }
 
-int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
-    auto* S = (sw_shard_state*)ctx;
+int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
+             int32_t wc, const int32_t* caps) {
     hipStream_t st = S->h->stream;
     const int64_t M = S->P * S->world;
+    const int32_t* capsd = nullptr;
+    if (mode == 5) {
+        memcpy(S->hcaps.p, caps, (size_t)S->T * 4);
+        SH_HIP(S, hipMemcpyAsync(S->caps.p, S->hcaps.p, (size_t)S->T * 4, hipMemcpyHostToDevice, st));
+        capsd = S->caps.p;
+    }
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
-           S->psend.p);
+           (int)wc, S->psend.p);
     SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr));
     SH_HIP(S, hipMemsetAsync(S->prank.p, 0, (size_t)M * 4, st));
     dim3 g2((unsigned)((M + kTB * kRankPer - 1) / (kTB * kRankPer)),
@@ -804,15 +838,43 @@ int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32
     uint64_t* yd = S->y[ydst].p;
     int32_t* pd = S->arr[pdst].p;
     if (M <= 2 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
+        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
     else if (M <= 8 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
+        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
     else if (M <= 32 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
+        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
     else if (M <= 64 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd);
+        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
     else
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
+    if (mode == 5) SH_HIP(S, hipStreamSynchronize(st)); /* hcaps is reused by the next class */
+    return SW_OK;
+}
+
+int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
+    return pack_any((sw_shard_state*)ctx, mode, src, Mb, ydst, pdst, 0, nullptr);
+}
+
+int op_pack_class(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
+                  int32_t pdst) {
+    return pack_any((sw_shard_state*)ctx, 5, src, 0.0, ydst, pdst, wc, caps);
+}
+
+int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps, int32_t* next_w) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 65));
+    LAUNCH(S, k_class_caps, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p,
+           S->y[ysrc].p, (int)wc);
+    int64_t cnt[64];
+    uint64_t nx = 0;
+    SH_TRY(coll_reduce(S, S->red.p, S->T, 0, cnt));
+    SH_TRY(coll_reduce(S, S->red.p + 64, 1, 1, &nx));
+    for (int t = 0; t < S->T; ++t) caps[t] = (int32_t)cnt[t];
+    *next_w = nx == 0 ? 0x7FFFFFFF : (int32_t)(0xFFFFFFFFull - nx);
     return SW_OK;
 }
 
@@ -838,7 +900,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
                S->planned.reserve(NL) || S->red.reserve(kRed) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
                S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
-               S->porder.reserve(M);
+               S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
     if (bad || S->hx.reserve(std::max<size_t>(xbytes * S->world, kRed * 8)))
@@ -901,6 +963,7 @@ void sw_shard_release(sw_handle* h) {
     S->planned.release(); S->prank.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
+    S->caps.release(); S->hcaps.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
@@ -990,6 +1053,8 @@ int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset
     ops.copy = op_copy;
     ops.copy_y = op_copy_y;
     ops.pack = op_pack;
+    ops.class_caps = op_class_caps;
+    ops.pack_class = op_pack_class;
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,
                             &res->p2_objective, &res->bound, &res->iters, &res->status);

@@ -48,10 +48,14 @@ def main():
     ap.add_argument("--policies", default="shockwave,max_min_fairness")
     ap.add_argument("--max-jobs", type=int, default=None)
     ap.add_argument("--time-per-iteration", type=int, default=120)
+    ap.add_argument("--future-rounds", type=int, default=None,
+                    help="override the config's T (BASELINE C3 uses 30 with the 256-GPU config)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg_name = f"scale_{max(64, a.gpus)}gpus.json"
     cfg = json.load(open(os.path.join(ROOT, "data", "configs", cfg_name)))
+    if a.future_rounds:
+        cfg["future_rounds"] = a.future_rounds
     trace = os.path.join(ROOT, "data", "traces", a.trace)
     if a.solver == "gpu":
         import sw_native as sn
@@ -66,6 +70,7 @@ def main():
             import milp_ref
             solver = milp_ref.MilpSolver()
     out = {"trace": a.trace, "gpus": a.gpus, "solver": a.solver, "config": cfg_name,
+           "future_rounds": cfg["future_rounds"],
            "time_per_iteration": a.time_per_iteration, "runs": {}}
     for pol in a.policies.split(","):
         t0 = time.time()
