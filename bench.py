@@ -68,7 +68,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="instances per GPU per step")
+    ap.add_argument("--batch", type=int, default=2048,
+                    help="instances per GPU per step (4 per workgroup slot: 2 slots per CU × 256 "
+                         "CUs, so per-instance work differences average out, DESIGN.md §6)")
     ap.add_argument("--jobs", type=int, default=900)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--seed", type=int, default=0)

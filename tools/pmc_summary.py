@@ -24,7 +24,7 @@ def per_kernel(path, grid_min):
 
 def main():
     tag, stats, fetch, write, sq = sys.argv[1:6]
-    grid_min = 512 * 64
+    grid_min = (int(sys.argv[6]) if len(sys.argv) > 6 else 512) * 512
     f, nf = per_kernel(fetch, grid_min)
     w, nw = per_kernel(write, grid_min)
     s, ns = per_kernel(sq, grid_min)
