@@ -428,19 +428,27 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     uint32_t* k2 = (uint32_t*)malloc(sizeof(uint32_t) * NN);
     int32_t* nbest = (int32_t*)malloc(sizeof(int32_t) * NN);
     double bound = 0.0, Jbest = 0.0;
+    int dens_best = 0; /* the best P1 plan is the density-order pack */
     for (int it = 0; it < SW_REPACK_ITERS; ++it) {
         double b0 = level_search(&P, n, nb, l, tk, tmp);
         if (it == 0) bound = b0;
         double Mb = 0.0;
         for (int32_t j = 0; j < N; ++j) Mb = sw_max(Mb, sw_g(&P.jc[j], nb[j]));
-        /* two packing orders: A = (critical level, key), B = (critical level,
-         * width, key); critical = losing the last round raises the makespan
-         * (only meaningful when k > 0).  Keep the better packed plan. */
+        /* packing orders: first P2's density order p_j/(n_j·w_j) — when it
+         * places every round it is also the P2 placement (same counts, same
+         * order) and the solve needs no other pack; otherwise A = (critical
+         * level, key) and B = (critical level, width, key), where critical =
+         * losing the last round raises the makespan (only meaningful when
+         * k > 0).  Keep the better packed plan of A and B. */
         int64_t deficit = 0;
         double Jp = 0.0;
-        for (int ord = 0; ord < 2; ++ord) {
+        int dens = 0;
+        for (int ord = -1; ord < 2; ++ord) {
             for (int32_t j = 0; j < N; ++j) {
-                if (nb[j] > 0) {
+                if (ord < 0) {
+                    k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] / (double)(nb[j] * P.jc[j].w)) : 0;
+                    k2[j] = 0;
+                } else if (nb[j] > 0) {
                     double lvl = sw_g(&P.jc[j], nb[j] - 1);
                     int crit = P.k > 0.0 && lvl > Mb;
                     k1[j] = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (ord ? (uint64_t)P.jc[j].w : 0);
@@ -449,10 +457,10 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
                     k1[j] = 0; k2[j] = 0;
                 }
             }
-            pack(&P, nb, k1, k2, ord ? y2 : y1, ord ? placed2 : placed, NULL, 0);
+            pack(&P, nb, k1, k2, ord == 1 ? y2 : y1, ord == 1 ? placed2 : placed, NULL, 0);
             int64_t dfc = 0;
             double Mp = 0.0;
-            const int32_t* pl = ord ? placed2 : placed;
+            const int32_t* pl = ord == 1 ? placed2 : placed;
             for (int32_t j = 0; j < N; ++j) {
                 dfc += (int64_t)P.jc[j].w * (nb[j] - pl[j]);
                 tmp[j] = fval(&P, j, pl[j]);
@@ -460,6 +468,10 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
             }
             double Jo = sw_detsum(tmp, N) - P.k * Mp;
             P.passes++;
+            if (ord < 0) {
+                if (dfc == 0) { Jp = Jo; dens = 1; break; }
+                continue;
+            }
             if (ord == 0 || Jo > Jp) {
                 Jp = Jo;
                 deficit = dfc;
@@ -472,6 +484,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         }
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
+            dens_best = dens;
             memcpy(nbest, placed, sizeof(int32_t) * NN);
             memcpy(ybest, y1, NN * (size_t)T);
         }
@@ -492,6 +505,10 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
      *       places every round);
      * and the P1 placement if none does (shockwave.py:325-326). ---- */
     int ok2 = 0;
+    if (dens_best) { /* (a) is the P1 placement itself */
+        memcpy(y2, y1, NN * (size_t)T);
+        ok2 = 1;
+    }
     for (int att = 0; att < 2 && !ok2; ++att) {
         for (int32_t j = 0; j < N; ++j) {
             k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] /

@@ -895,16 +895,18 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     int64_t deficit = 0;
     int it = 0, mode = 0; /* mode 0 = run the level search next */
     bool ok2 = true;
+    bool dens = false, dens_best = false; /* P1 placed by the density order */
     while (true) {
         if (mode == 0) {
             const double b0 = c.level_search();
             if (it == 0) bound = b0;
             SW_STAMP(1);
-            mode = 1;
+            mode = 4; /* P1 orders: density, then A (1), then B (3) */
+            dens = false;
         }
         if (mode == 2) break; /* P2 below */
         uint8_t* pl = (mode == 3) ? c.placed2 : c.placed;
-        uint64_t* yd = (mode == 1) ? c.ycur : c.y2;
+        uint64_t* yd = (mode == 3) ? c.y2 : c.ycur;
         c.pack(mode, c.nbest, yd, pl);
         int64_t def_l = 0;
         double fs = 0.0, gm = 0.0;
@@ -918,7 +920,12 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.blk.detsum_max(fs, gm, U, Mx);
         const double Jo = U - c.k * Mx;
         c.passes++;
-        if (mode == 1 || Jo > Jp) {
+        if (mode == 4) { /* density order: also the P2 placement when it packs */
+            if (dfc != 0) { mode = 1; continue; }
+            Jp = Jo;
+            deficit = 0;
+            dens = true;
+        } else if (mode == 1 || Jo > Jp) {
             Jp = Jo;
             deficit = dfc;
             if (mode == 3) {
@@ -934,6 +941,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         SW_STAMP(2);
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
+            dens_best = dens;
             c.for_jobs([&](int j, int s) {
                 (void)s;
                 c.nfin[j] = c.placed[j];
@@ -960,6 +968,10 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         return c.blk.sum(bad_l) == 0;
     };
     ok2 = false;
+    if (dens_best) { /* (a) is the P1 placement itself */
+        c.for_jobs([&](int j, int s) { (void)s; c.y2[j] = c.ybest[j]; });
+        ok2 = true;
+    }
     for (int att = 0; att < 2 && !ok2; ++att) {
         c.pack(att == 0 ? 4 : 2, c.nfin, c.y2, c.placed);
         ok2 = p2_ok();

@@ -329,6 +329,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         c->steps++;
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
+        int dens_best = 0;
         int64_t isum;
         for (int it = 0; it < SW_REPACK_ITERS; ++it) {
             double b0;
@@ -339,14 +340,20 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             c->steps++;
             int64_t deficit = 0;
             double Jp = 0.0;
-            for (int ord = 0; ord < 2; ++ord) {
-                const int32_t pdst = ord ? SW_A_PL2 : SW_A_PL;
-                SWC_RUN(o->pack(o->ctx, ord ? 3 : 1, SW_A_NB, Mb, ord ? SW_Y_2 : SW_Y_CUR, pdst));
+            int dens = 0;
+            for (int ord = -1; ord < 2; ++ord) {
+                const int32_t pdst = ord == 1 ? SW_A_PL2 : SW_A_PL;
+                const int32_t pm = ord < 0 ? 4 : ord ? 3 : 1;
+                SWC_RUN(o->pack(o->ctx, pm, SW_A_NB, Mb, ord == 1 ? SW_Y_2 : SW_Y_CUR, pdst));
                 c->steps++;
                 int64_t dfc;
                 SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, pdst, c->lanesA, c->lanesB, &gm, &dfc));
                 c->steps++;
                 const double Jo = sw_shard_tree(c->lanesA) - c->k * gm;
+                if (ord < 0) { /* density order: also the P2 placement when it packs */
+                    if (dfc == 0) { Jp = Jo; dens = 1; break; }
+                    continue;
+                }
                 if (ord == 0 || Jo > Jp) {
                     Jp = Jo;
                     deficit = dfc;
@@ -359,6 +366,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             }
             if (it == 0 || Jp > Jbest) {
                 Jbest = Jp;
+                dens_best = dens;
                 SWC_RUN(o->copy(o->ctx, SW_A_NFIN, SW_A_PL));
                 SWC_RUN(o->copy_y(o->ctx, SW_Y_BEST, SW_Y_CUR));
             }
@@ -371,6 +379,10 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
          * profile — first that places every round (twin: the P2 block) */
         int ok2 = 0;
         int64_t bad;
+        if (dens_best) { /* (a) is the P1 placement itself */
+            SWC_RUN(o->copy_y(o->ctx, SW_Y_2, SW_Y_BEST));
+            ok2 = 1;
+        }
         for (int att = 0; att < 2 && !ok2; ++att) {
             SWC_RUN(o->pack(o->ctx, att == 0 ? 4 : 2, SW_A_NFIN, 0.0, SW_Y_2, SW_A_PL));
             c->steps++;
