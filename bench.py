@@ -33,6 +33,15 @@ import sw_synth as ss  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 
+# The result line is the only thing on stdout: libraries (RCCL prints its
+# version banner on communicator init) write to fd 1 directly, so fd 1 is
+# pointed at stderr and the JSON line goes to a saved copy of the real stdout.
+_RESULT_OUT = None
+
+
+def emit(line: dict):
+    print(json.dumps(line), file=_RESULT_OUT or sys.stdout, flush=True)
+
 
 def pass_bytes(N: int, T: int) -> int:
     """Algorithmic bytes of one pass of the plan kernel over an instance's jobs.
@@ -69,8 +78,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=2048,
-                    help="instances per GPU per step (4 per workgroup slot: 2 slots per CU × 256 "
-                         "CUs, so per-instance work differences average out, DESIGN.md §6)")
+                    help="instances per GPU per step (8 per CU: one 512-thread workgroup fits a "
+                         "CU at a time, so per-instance work differences average out, DESIGN.md §6)")
     ap.add_argument("--jobs", type=int, default=900)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--seed", type=int, default=0)
@@ -164,13 +173,17 @@ def main_c4(args, world, rank, local, dist):
             "collective_steps": r["iters"],
             "objective": r["objective"],
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     solver.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
 def main():
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -289,7 +302,7 @@ def main():
             "single_instance_ms": lat_ms,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     solver.close()
     if dist is not None:
         dist.destroy_process_group()

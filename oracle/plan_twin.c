@@ -93,6 +93,7 @@ static int32_t cnt_ge(const twin_t* P, int32_t j, uint32_t rho, int32_t l) {
 
 typedef struct {
     double U, Mact, J, ubound;
+    uint32_t rho; /* price ρ* bits (0 when every item fits) */
 } sel_eval_t;
 
 /*
@@ -101,8 +102,13 @@ typedef struct {
  * C − Σ w l, computed as a price threshold ρ* (bisection over fp32 key bits),
  * the job-ordered tie group at ρ*, and a ≤7-unit width tail.  is_inf: M = +∞.
  */
+/* [plo, phi]: a bracket of ρ*(M) from already evaluated levels — ρ* is
+ * non-increasing in M (a larger level frees forced rounds, and the budget
+ * grows by exactly their weight), so ρ*(M') ≤ ρ*(M) ≤ ρ*(M'') for
+ * M'' < M < M'.  The bisection returns the same ρ* from any valid bracket. */
 static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
-                        int32_t* taken, double* tmp, sel_eval_t* ev) {
+                        int32_t* taken, double* tmp, sel_eval_t* ev, uint32_t plo,
+                        uint32_t phi) {
     const int32_t N = P->N;
     int64_t Wf = 0, Wall = 0;
     for (int32_t j = 0; j < N; ++j) {
@@ -115,11 +121,12 @@ static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
     int64_t bud = P->C - Wf;
     double rho_d = 0.0;
     int64_t wgt_star = 0;
+    ev->rho = 0;
     if (Wall <= bud) {
         for (int32_t j = 0; j < N; ++j) { n[j] = P->Tj[j]; taken[j] = P->Tj[j] - l[j]; }
         wgt_star = Wall;
     } else {
-        uint32_t lo = 0, hi = SW_KEY_INF_BITS;
+        uint32_t lo = plo, hi = phi;
         while (lo < hi) {
             uint32_t mid = lo + ((hi - lo) >> 1);
             int64_t wg = 0;
@@ -128,6 +135,7 @@ static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
             if (wg <= bud) hi = mid; else lo = mid + 1;
         }
         uint32_t rho = lo;
+        ev->rho = rho;
         rho_d = (double)sw_float_of(rho);
         int64_t wt = 0;
         for (int32_t j = 0; j < N; ++j) {
@@ -363,8 +371,9 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
     const int32_t N = P->N;
     size_t NN = N > 0 ? (size_t)N : 1;
     sel_eval_t ev, best;
-    select_level(P, 0.0, 1, n, l, tk, tmp, &ev);
+    select_level(P, 0.0, 1, n, l, tk, tmp, &ev, 0, SW_KEY_INF_BITS);
     best = ev;
+    const uint32_t rho_inf = ev.rho; /* ρ*(+∞): a lower bound at every level */
     double U_inf = ev.U, M_free = ev.Mact, ubound_inf = ev.ubound;
     memcpy(nb, n, sizeof(int32_t) * NN);
     double M_lo = M_free;
@@ -377,27 +386,43 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
             if (feasible_level(P, sw_from_bits(mid))) hi = mid; else lo = mid + 1;
         }
         M_lo = sw_from_bits(lo);
-        select_level(P, M_lo, 0, n, l, tk, tmp, &ev);
+        select_level(P, M_lo, 0, n, l, tk, tmp, &ev, rho_inf, SW_KEY_INF_BITS);
         if (ev.J > best.J || (ev.J == best.J && ev.Mact < best.Mact)) {
             best = ev; memcpy(nb, n, sizeof(int32_t) * NN);
         }
+        /* golden-section search on [a, b] that reuses the surviving interior
+         * point (one new level per shrink); every probe's price is bracketed
+         * by its evaluated neighbours (a and the other interior point, or b) */
         double width = (U_inf - ev.U) / P->k;
         double a = M_lo, b = sw_min(M_free, M_lo + width);
-        for (int it = 0; it < SW_GS_ITERS; ++it) {
-            if (!(a < b)) break;
-            if (levels_between(P, a, b) == 0) break;
+        uint32_t ra = ev.rho, rb = rho_inf; /* ρ*(a); a lower bound of ρ*(b) */
+        if (a < b && levels_between(P, a, b) > 0) {
             double m1 = a + (b - a) * SW_GS_A;
             double m2 = a + (b - a) * SW_GS_B;
             sel_eval_t e1, e2;
-            select_level(P, m1, 0, n, l, tk, tmp, &e1);
+            select_level(P, m1, 0, n, l, tk, tmp, &e1, rb, ra);
             if (e1.J > best.J || (e1.J == best.J && e1.Mact < best.Mact)) {
                 best = e1; memcpy(nb, n, sizeof(int32_t) * NN);
             }
-            select_level(P, m2, 0, n, l, tk, tmp, &e2);
+            select_level(P, m2, 0, n, l, tk, tmp, &e2, rb, e1.rho);
             if (e2.J > best.J || (e2.J == best.J && e2.Mact < best.Mact)) {
                 best = e2; memcpy(nb, n, sizeof(int32_t) * NN);
             }
-            if (e1.J >= e2.J) b = m2; else a = m1;
+            for (int it = 0; it < SW_GS_ITERS; ++it) {
+                const int left = e1.J >= e2.J;
+                if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
+                else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
+                if (!(a < b)) break;
+                if (levels_between(P, a, b) == 0) break;
+                sel_eval_t* e = left ? &e1 : &e2;
+                double m;
+                if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
+                else { m2 = a + (b - a) * SW_GS_B; m = m2; }
+                select_level(P, m, 0, n, l, tk, tmp, e, left ? e2.rho : rb, left ? ra : e1.rho);
+                if (e->J > best.J || (e->J == best.J && e->Mact < best.Mact)) {
+                    best = *e; memcpy(nb, n, sizeof(int32_t) * NN);
+                }
+            }
         }
     }
     return ubound_inf - P->k * M_lo;

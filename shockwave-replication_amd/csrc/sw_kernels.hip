@@ -54,6 +54,7 @@ namespace {
 
 struct SelEval {
     double U, Mact, J, ubound;
+    uint32_t rho; /* price ρ* bits of the level (0 when every item fits) */
 };
 
 /* packed per-position packer state: r | w << 8 | sel << 16 */
@@ -258,7 +259,10 @@ struct Ctx {
     }
 
     /* twin: select_level */
-    __device__ __forceinline__ SelEval select_level(double M, bool is_inf) {
+    /* [plo, phi] brackets ρ*(M) from evaluated neighbour levels (twin:
+     * select_level); ev.rho returns ρ* (0 when every item fits) */
+    __device__ __forceinline__ SelEval select_level(double M, bool is_inf, uint32_t plo,
+                                                    uint32_t phi) {
         int64_t wf = 0, wall = 0;
         for_jobs([&](int j, int s) {
             const int l = is_inf ? 0 : lforce(j, s, M);
@@ -270,6 +274,7 @@ struct Ctx {
         blk.sum2(wf, wall, Wf, Wall);
         passes++;
         SelEval ev;
+        ev.rho = 0;
         if (Wf > C) {
             ev.U = 0; ev.Mact = 0; ev.J = -1e308; ev.ubound = 0;
             return ev;
@@ -284,7 +289,7 @@ struct Ctx {
             });
             wgt_star = Wall;
         } else {
-            uint32_t lo = 0, hi = SW_KEY_INF_BITS;
+            uint32_t lo = plo, hi = phi;
             while (lo < hi) {
                 const uint32_t mid = lo + ((hi - lo) >> 1);
                 int32_t wg = 0;
@@ -294,6 +299,7 @@ struct Ctx {
                 if (wg <= bud) hi = mid; else lo = mid + 1;
             }
             const uint32_t rho = lo;
+            ev.rho = rho;
             rho_d = (double)sw_float_of(rho);
             int64_t wt_l = 0;
             int32_t tie_l = 0;
@@ -389,19 +395,24 @@ struct Ctx {
      * Written as a loop over evaluation requests so select_level has a
      * single call site (phase 0: M = +inf; 1: M = M_lo; 2/3: golden m1/m2). */
     __device__ __forceinline__ double level_search() {
-        SelEval best, e1;
+        SelEval best, e1, e2;
         best.U = best.Mact = best.ubound = 0.0;
         best.J = -1e308;
+        best.rho = 0;
         e1 = best;
+        e2 = best;
         double U_inf = 0.0, M_free = 0.0, ub_inf = 0.0, M_lo = 0.0;
         double a = 0.0, b = 0.0, m1 = 0.0, m2 = 0.0;
+        uint32_t rho_inf = 0, ra = 0, rb = 0, plo = 0, phi = SW_KEY_INF_BITS;
+        /* phase 0: M = +inf; 1: M_lo; 2 / 3: the first golden pair m1, m2;
+         * 4 / 5: the new m1 / m2 after a shrink that kept the other point */
         int phase = 0, it = 0;
         while (true) {
             double M = 0.0;
             if (phase == 1) M = M_lo;
-            else if (phase == 2) M = m1;
-            else if (phase == 3) M = m2;
-            const SelEval ev = select_level(M, phase == 0);
+            else if (phase == 2 || phase == 4) M = m1;
+            else if (phase >= 3) M = m2;
+            const SelEval ev = select_level(M, phase == 0, plo, phi);
             if (phase == 0) {
                 best = ev;
                 for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
@@ -409,6 +420,7 @@ struct Ctx {
                 M_free = ev.Mact;
                 ub_inf = ev.ubound;
                 M_lo = M_free;
+                rho_inf = ev.rho;
                 if (!(N > 0 && k > 0.0)) break;
                 double lb = 0.0;
                 for_jobs([&](int j, int s) { lb = sw_max(lb, gval(j, s, Tj(j, s))); });
@@ -419,6 +431,8 @@ struct Ctx {
                     if (feasible_level(sw_from_bits(mid))) hi = mid; else lo = mid + 1;
                 }
                 M_lo = sw_from_bits(lo);
+                plo = rho_inf;
+                phi = SW_KEY_INF_BITS;
                 phase = 1;
                 continue;
             }
@@ -427,21 +441,45 @@ struct Ctx {
                 const double width = (U_inf - ev.U) / k;
                 a = M_lo;
                 b = sw_min(M_free, M_lo + width);
+                ra = ev.rho;
+                rb = rho_inf;
                 it = 0;
-            } else if (phase == 2) {
+                if (!(a < b)) break;
+                if (levels_between(a, b) == 0) break;
+                m1 = a + (b - a) * SW_GS_A;
+                m2 = a + (b - a) * SW_GS_B;
+                plo = rb;
+                phi = ra;
+                phase = 2;
+                continue;
+            }
+            if (phase == 2) {
                 e1 = ev;
+                plo = rb;
+                phi = e1.rho;
                 phase = 3;
                 continue;
-            } else {
-                if (e1.J >= ev.J) b = m2; else a = m1;
-                ++it;
             }
-            /* next golden-section pair, if any */
-            if (it >= SW_GS_ITERS || !(a < b)) break;
+            if (phase == 4) e1 = ev; else e2 = ev; /* phases 3, 5 */
+            /* golden-section shrink that keeps the surviving interior point */
+            if (it >= SW_GS_ITERS) break;
+            const bool left = e1.J >= e2.J;
+            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
+            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
+            ++it;
+            if (!(a < b)) break;
             if (levels_between(a, b) == 0) break;
-            m1 = a + (b - a) * SW_GS_A;
-            m2 = a + (b - a) * SW_GS_B;
-            phase = 2;
+            if (left) {
+                m1 = a + (b - a) * SW_GS_A;
+                plo = e2.rho;
+                phi = ra;
+                phase = 4;
+            } else {
+                m2 = a + (b - a) * SW_GS_B;
+                plo = rb;
+                phi = e1.rho;
+                phase = 5;
+            }
         }
         __syncthreads();
         return ub_inf - k * M_lo;

@@ -155,6 +155,7 @@ typedef struct {
 
 typedef struct {
     double U, Mact, J, ubound;
+    uint32_t rho; /* price ρ* bits (0 when every item fits) */
 } sw_shard_eval;
 
 #define SWC_TRY(x)              \
@@ -202,13 +203,15 @@ static inline int swc_search(sw_shard_ctl* c, int kind, uint64_t lo, uint64_t hi
     return 0;
 }
 
-/* twin: select_level */
-static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eval* ev) {
+/* twin: select_level ([plo, phi] brackets ρ*(M), see there) */
+static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eval* ev,
+                             uint32_t plo, uint32_t phi) {
     const sw_shard_ops* o = c->ops;
     int64_t wfa[2];
     SWC_TRY(o->force(o->ctx, M, is_inf, wfa));
     c->steps++;
     const int64_t Wf = wfa[0], Wall = wfa[1];
+    ev->rho = 0;
     if (Wf > c->C) {
         ev->U = 0.0; ev->Mact = 0.0; ev->J = -1e308; ev->ubound = 0.0;
         return 0;
@@ -221,8 +224,9 @@ static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eva
         wgt_star = Wall;
     } else {
         uint64_t r64;
-        SWC_TRY(swc_search(c, 0, 0, SW_KEY_INF_BITS, bud, &r64));
+        SWC_TRY(swc_search(c, 0, plo, phi, bud, &r64));
         const uint32_t rho = (uint32_t)r64;
+        ev->rho = rho;
         rho_d = (double)sw_float_of(rho);
         int64_t wt, excl, used;
         SWC_TRY(o->take(o->ctx, rho, &wt, &excl));
@@ -265,8 +269,9 @@ static inline int swc_keep(sw_shard_ctl* c, const sw_shard_eval* e, sw_shard_eva
 static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
     const sw_shard_ops* o = c->ops;
     sw_shard_eval ev, best;
-    SWC_TRY(swc_select(c, 0.0, 1, &ev));
+    SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, SW_KEY_INF_BITS));
     best = ev;
+    const uint32_t rho_inf = ev.rho;
     const double U_inf = ev.U, M_free = ev.Mact, ub_inf = ev.ubound;
     SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
     double M_lo = M_free;
@@ -274,24 +279,40 @@ static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
         uint64_t lo;
         SWC_TRY(swc_search(c, 1, sw_bits(c->lb), sw_bits(M_free), c->C, &lo));
         M_lo = sw_from_bits(lo);
-        SWC_TRY(swc_select(c, M_lo, 0, &ev));
+        SWC_TRY(swc_select(c, M_lo, 0, &ev, rho_inf, SW_KEY_INF_BITS));
         SWC_TRY(swc_keep(c, &ev, &best));
+        /* golden section with the surviving interior point reused (twin) */
         const double width = (U_inf - ev.U) / c->k;
         double a = M_lo, b = sw_min(M_free, M_lo + width);
-        for (int it = 0; it < SW_GS_ITERS; ++it) {
-            if (!(a < b)) break;
-            int64_t nbw;
+        uint32_t ra = ev.rho, rb = rho_inf;
+        int64_t nbw = 0;
+        if (a < b) {
             SWC_TRY(o->between(o->ctx, a, b, &nbw));
             c->steps++;
-            if (nbw == 0) break;
-            const double m1 = a + (b - a) * SW_GS_A;
-            const double m2 = a + (b - a) * SW_GS_B;
+        }
+        if (a < b && nbw > 0) {
+            double m1 = a + (b - a) * SW_GS_A;
+            double m2 = a + (b - a) * SW_GS_B;
             sw_shard_eval e1, e2;
-            SWC_TRY(swc_select(c, m1, 0, &e1));
+            SWC_TRY(swc_select(c, m1, 0, &e1, rb, ra));
             SWC_TRY(swc_keep(c, &e1, &best));
-            SWC_TRY(swc_select(c, m2, 0, &e2));
+            SWC_TRY(swc_select(c, m2, 0, &e2, rb, e1.rho));
             SWC_TRY(swc_keep(c, &e2, &best));
-            if (e1.J >= e2.J) b = m2; else a = m1;
+            for (int it = 0; it < SW_GS_ITERS; ++it) {
+                const int left = e1.J >= e2.J;
+                if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
+                else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
+                if (!(a < b)) break;
+                SWC_TRY(o->between(o->ctx, a, b, &nbw));
+                c->steps++;
+                if (nbw == 0) break;
+                sw_shard_eval* e = left ? &e1 : &e2;
+                double m;
+                if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
+                else { m2 = a + (b - a) * SW_GS_B; m = m2; }
+                SWC_TRY(swc_select(c, m, 0, e, left ? e2.rho : rb, left ? ra : e1.rho));
+                SWC_TRY(swc_keep(c, e, &best));
+            }
         }
     }
     *bound = ub_inf - c->k * M_lo;
