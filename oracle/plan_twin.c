@@ -454,6 +454,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     int32_t* nbest = (int32_t*)malloc(sizeof(int32_t) * NN);
     double bound = 0.0, Jbest = 0.0;
     int dens_best = 0; /* the best P1 plan is the density-order pack */
+    int dskip_best = 0; /* density failed on exactly the final counts: P2 (a) would too */
     for (int it = 0; it < SW_REPACK_ITERS; ++it) {
         double b0 = level_search(&P, n, nb, l, tk, tmp);
         if (it == 0) bound = b0;
@@ -510,6 +511,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             dens_best = dens;
+            dskip_best = !dens && deficit == 0;
             memcpy(nbest, placed, sizeof(int32_t) * NN);
             memcpy(ybest, y1, NN * (size_t)T);
         }
@@ -535,6 +537,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         ok2 = 1;
     }
     for (int att = 0; att < 2 && !ok2; ++att) {
+        if (att == 0 && dskip_best) continue;
         for (int32_t j = 0; j < N; ++j) {
             k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] /
                                         (double)(att == 0 ? nb[j] * P.jc[j].w : nb[j]))

@@ -934,6 +934,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     int it = 0, mode = 0; /* mode 0 = run the level search next */
     bool ok2 = true;
     bool dens = false, dens_best = false; /* P1 placed by the density order */
+    bool dskip_best = false; /* density failed on exactly the final counts */
     while (true) {
         if (mode == 0) {
             const double b0 = c.level_search();
@@ -980,6 +981,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             dens_best = dens;
+            dskip_best = !dens && deficit == 0;
             c.for_jobs([&](int j, int s) {
                 (void)s;
                 c.nfin[j] = c.placed[j];
@@ -1011,6 +1013,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         ok2 = true;
     }
     for (int att = 0; att < 2 && !ok2; ++att) {
+        if (att == 0 && dskip_best) continue;
         c.pack(att == 0 ? 4 : 2, c.nfin, c.y2, c.placed);
         ok2 = p2_ok();
         if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;

@@ -350,7 +350,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         c->steps++;
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
-        int dens_best = 0;
+        int dens_best = 0, dskip_best = 0;
         int64_t isum;
         for (int it = 0; it < SW_REPACK_ITERS; ++it) {
             double b0;
@@ -388,6 +388,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             if (it == 0 || Jp > Jbest) {
                 Jbest = Jp;
                 dens_best = dens;
+                dskip_best = !dens && deficit == 0;
                 SWC_RUN(o->copy(o->ctx, SW_A_NFIN, SW_A_PL));
                 SWC_RUN(o->copy_y(o->ctx, SW_Y_BEST, SW_Y_CUR));
             }
@@ -405,6 +406,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             ok2 = 1;
         }
         for (int att = 0; att < 2 && !ok2; ++att) {
+            if (att == 0 && dskip_best) continue;
             SWC_RUN(o->pack(o->ctx, att == 0 ? 4 : 2, SW_A_NFIN, 0.0, SW_Y_2, SW_A_PL));
             c->steps++;
             SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
