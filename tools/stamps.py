@@ -22,7 +22,7 @@ def main():
     lib = sn.load(os.path.join(ROOT, "shockwave-replication_amd", "lib", "libshockwave_amd_stamps.so"))
     lib.sw_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     cases = {
-        "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 64)],
+        "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] != "-v" else 64)],
         "g64_900x20_k1e-3": [ss.synth_problem(i, 900, 64, 20, 120.0, 1e-3, 15.0) for i in range(16)],
         "g128_120x20_k10": [ss.synth_problem(i, 120, 128, 20, 120.0, 10.0, 5.0) for i in range(16)],
     }
@@ -40,6 +40,9 @@ def main():
               f"status {sorted(set(r['status'] for r in res))}")
         for i, n in enumerate(names):
             print(f"   {n:16s} {st[:, i].mean():12.0f}  {100 * st[:, i].mean() / tot:5.1f}%")
+        if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
+            for r, row in list(zip(res, st))[:24]:
+                print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row))
         s.close()
 
 
