@@ -55,6 +55,7 @@ namespace {
 
 constexpr int kTB = 256;  /* threads per block of the per-job kernels */
 constexpr int kRed = 128; /* entries of the step-result buffer        */
+constexpr int kRing = 64; /* step-result slices cleared together      */
 
 struct sw_pack_ent {
     uint64_t khi, klo; /* order key (desc); klo low 32 bits = ~job */
@@ -432,6 +433,18 @@ __global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* s
     red_umax(S.red + 64, nx);
 }
 
+/* per-solve state: every count array, every bitmask, l and taken = 0 */
+__global__ __launch_bounds__(kTB) void k_zero_state(ShardDev S) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.NL) return;
+#pragma unroll
+    for (int a = 0; a < SW_A_COUNT; ++a) S.arr[a][i] = 0;
+#pragma unroll
+    for (int a = 0; a < SW_Y_COUNT; ++a) S.y[a][i] = 0;
+    S.l[i] = 0;
+    S.taken[i] = 0;
+}
+
 /* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') >
  * key(e)}.  Keys are unique (they end in ~job), so the ranks of the active
  * entries are a permutation of [0, A).  A block ranks kRankPer·kTB entries
@@ -555,6 +568,8 @@ struct sw_shard_state {
     DevBuf<long long> red;
     DevBuf<sw_pack_ent> psend, pall;
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
+    int ring_pos = kRing; /* next step-result slice (kRing = clear the ring first) */
+    bool zero_pending = false;
     /* pinned staging */
     HostBuf<uint8_t> hx;
     HostBuf<int32_t> hcaps;
@@ -598,7 +613,7 @@ int host_fail(sw_shard_state* S, const char* what) {
 int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
     hipStream_t st = S->h->stream;
     const size_t bytes = (size_t)n * 8;
-    if (S->comm) {
+    if (S->comm && S->world > 1) { /* one rank: the reduction is the identity */
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
@@ -620,15 +635,18 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
     hipStream_t st = S->h->stream;
     const size_t total = bytes * (size_t)S->world;
     if (!S->host_comm) {
-        if (!S->comm) {
-            if (drecv != dsend)
+        const bool one = !S->comm || S->world == 1;
+        /* one rank: the gather is the identity; a gather read back by the host
+         * is not needed on the device afterwards, so it is copied down directly */
+        if (one) {
+            if (drecv != dsend && !hrecv)
                 SH_HIP(S, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, st));
         } else {
             SH_NCCL(S, ncclAllGather(dsend, drecv, bytes, ncclUint8, S->comm, st));
         }
         if (hrecv) {
             if (S->hx.reserve(total)) return host_fail(S, "pinned staging");
-            SH_HIP(S, hipMemcpyAsync(S->hx.p, drecv, total, hipMemcpyDeviceToHost, st));
+            SH_HIP(S, hipMemcpyAsync(S->hx.p, one ? dsend : drecv, total, hipMemcpyDeviceToHost, st));
             SH_HIP(S, hipStreamSynchronize(st));
             memcpy(hrecv, S->hx.p, total);
         }
@@ -649,8 +667,17 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
     return SW_OK;
 }
 
+/* Step-result slots: a ring of kRing zeroed slices of kRed entries.  Each
+ * step takes the next slice (S->dv.red, passed to its kernels by value), so
+ * the whole ring is cleared once per kRing steps instead of a memset per step. */
 int zero_red(sw_shard_state* S, int n) {
-    SH_HIP(S, hipMemsetAsync(S->red.p, 0, (size_t)n * 8, S->h->stream));
+    (void)n;
+    if (S->ring_pos >= kRing) {
+        SH_HIP(S, hipMemsetAsync(S->red.p, 0, (size_t)kRing * kRed * 8, S->h->stream));
+        S->ring_pos = 0;
+    }
+    S->dv.red = S->red.p + (size_t)S->ring_pos * kRed;
+    S->ring_pos++;
     return SW_OK;
 }
 
@@ -669,10 +696,10 @@ int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
     LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->w.p, S->d.p, S->F.p,
            S->E.p, S->R.p, S->delta);
     uint64_t mx[2];
-    SH_TRY(coll_reduce(S, S->red.p, 2, 1, mx));
+    SH_TRY(coll_reduce(S, S->dv.red, 2, 1, mx));
     if (S->host_comm && S->world > 1) { /* kernels read A from red[0] */
         memcpy(S->hx.p, mx, 16);
-        SH_HIP(S, hipMemcpyAsync(S->red.p, S->hx.p, 16, hipMemcpyHostToDevice, st));
+        SH_HIP(S, hipMemcpyAsync(S->dv.red, S->hx.p, 16, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipStreamSynchronize(st));
     }
     LAUNCH(S, k_keys, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv);
@@ -693,7 +720,7 @@ int op_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 2));
     LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, M, (int)is_inf);
-    return coll_reduce(S, S->red.p, 2, 0, out);
+    return coll_reduce(S, S->dv.red, 2, 0, out);
 }
 
 template <bool LEVEL>
@@ -704,7 +731,7 @@ int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
     SH_TRY(zero_red(S, K + 1));
     LAUNCH(S, k_probe<LEVEL>, dim3(nblk((int64_t)S->NL * S->T)), dim3(kTB), 0, S->h->stream, S->dv, th);
     int64_t bins[SW_SHARD_K + 1];
-    SH_TRY(coll_reduce(S, S->red.p, K + 1, 0, bins));
+    SH_TRY(coll_reduce(S, S->dv.red, K + 1, 0, bins));
     int64_t suf = 0;
     for (int i = K - 1; i >= 0; --i) { suf += bins[i + 1]; out[i] = suf; }
     return SW_OK;
@@ -726,7 +753,7 @@ int op_between(void* ctx, double a, double b, int64_t* out) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
     LAUNCH(S, k_between, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, a, b);
-    return coll_reduce(S, S->red.p, 1, 0, out);
+    return coll_reduce(S, S->dv.red, 1, 0, out);
 }
 
 int op_take_all(void* ctx) {
@@ -740,7 +767,7 @@ int op_take(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl) {
     SH_TRY(zero_red(S, 2));
     LAUNCH(S, k_take, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, rho);
     std::vector<int64_t> all((size_t)2 * S->world);
-    SH_TRY(coll_gather(S, S->red.p, S->xrecv.p, 16, all.data()));
+    SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 16, all.data()));
     *wt = 0;
     *excl = 0;
     for (int r = 0; r < S->world; ++r) {
@@ -756,14 +783,14 @@ int op_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used)
     (void)rho; /* k_take stored the tie counts at rho */
     LAUNCH(S, k_assign, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, (long long)rem,
            (long long)excl);
-    return coll_reduce(S, S->red.p, 1, 0, used);
+    return coll_reduce(S, S->dv.red, 1, 0, used);
 }
 
 int op_tail_best(void* ctx, int64_t rem2, uint64_t* best) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
     LAUNCH(S, k_tail_best, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (long long)rem2);
-    return coll_reduce(S, S->red.p, 1, 1, best);
+    return coll_reduce(S, S->dv.red, 1, 1, best);
 }
 
 int op_tail_apply(void* ctx, int64_t jb) {
@@ -871,8 +898,8 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* cap
            S->y[ysrc].p, (int)wc);
     int64_t cnt[64];
     uint64_t nx = 0;
-    SH_TRY(coll_reduce(S, S->red.p, S->T, 0, cnt));
-    SH_TRY(coll_reduce(S, S->red.p + 64, 1, 1, &nx));
+    SH_TRY(coll_reduce(S, S->dv.red, S->T, 0, cnt));
+    SH_TRY(coll_reduce(S, S->dv.red + 64, 1, 1, &nx));
     for (int t = 0; t < S->T; ++t) caps[t] = (int32_t)cnt[t];
     *next_w = nx == 0 ? 0x7FFFFFFF : (int32_t)(0xFFFFFFFFull - nx);
     return SW_OK;
@@ -897,7 +924,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
                S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
                S->l.reserve(NL) || S->taken.reserve(NL) || S->tie.reserve(NL) ||
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
-               S->planned.reserve(NL) || S->red.reserve(kRed) ||
+               S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
                S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
                S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64);
@@ -913,12 +940,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
         SH_HIP(S, hipMemcpyAsync(S->d.p, pr->epoch_duration, n * 8, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipMemcpyAsync(S->R.p, pr->remaining_runtime, n * 8, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipMemcpyAsync(S->p.p, pr->priority, n * 8, hipMemcpyHostToDevice, st));
-        for (int a = 0; a < SW_A_COUNT; ++a)
-            SH_HIP(S, hipMemsetAsync(S->arr[a].p, 0, n * 4, st));
-        for (int a = 0; a < SW_Y_COUNT; ++a)
-            SH_HIP(S, hipMemsetAsync(S->y[a].p, 0, n * 8, st));
-        SH_HIP(S, hipMemsetAsync(S->l.p, 0, n * 4, st));
-        SH_HIP(S, hipMemsetAsync(S->taken.p, 0, n * 4, st));
+        S->zero_pending = true; /* k_zero_state once the kernel view is built */
     }
     ShardDev& v = S->dv;
     memset(&v, 0, sizeof(v));
@@ -935,6 +957,11 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
     for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
     for (int a = 0; a < SW_Y_COUNT; ++a) v.y[a] = S->y[a].p;
     v.plan = S->plan.p; v.planned = S->planned.p; v.red = S->red.p;
+    S->ring_pos = kRing; /* the first step clears the ring */
+    if (S->zero_pending) {
+        LAUNCH(S, k_zero_state, dim3(nblk(S->NL)), dim3(kTB), 0, st, v);
+        S->zero_pending = false;
+    }
     return SW_OK;
 }
 
