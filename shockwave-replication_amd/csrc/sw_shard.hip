@@ -56,6 +56,7 @@ namespace {
 constexpr int kTB = 256;  /* threads per block of the per-job kernels */
 constexpr int kRed = 128; /* entries of the step-result buffer        */
 constexpr int kRing = 64; /* step-result slices cleared together      */
+constexpr int kProbeBlocks = 256; /* grid of the K-ary probe kernels       */
 
 struct sw_pack_ent {
     uint64_t khi, klo; /* order key (desc); klo low 32 bits = ~job */
@@ -188,16 +189,20 @@ __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
     if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
     if (threadIdx.x < th.K) thr[threadIdx.x] = th.v[threadIdx.x];
     __syncthreads();
-    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
-    if (e < (int64_t)S.NL * S.T) {
-        const int i = (int)(e / S.T), n = (int)(e % S.T);
-        const sw_jobc c = S.jc[i];
-        const int tj = tj_of(S, c);
+    /* grid-stride over the items (NL·T < 2^31): a bounded grid keeps the
+     * block → global flush at ≤ kProbeBlocks·K atomics per probe */
+    const int items = S.NL * S.T;
+    int32_t wtop = 0; /* items above every threshold: wave-summed, one atomic per wave */
+    for (int e = (int)blockIdx.x * kTB + (int)threadIdx.x; e < items; e += (int)gridDim.x * kTB) {
+        const int i = e / S.T, n = e - i * S.T;
+        const int32_t w = S.jc[i].w;
+        const int tj = w <= S.G ? S.T : 0;
         bool live;
         int lo = 0, hi = th.K;
         if (LEVEL) {
             live = n < tj;
             if (live) {
+                const sw_jobc c = S.jc[i];
                 const double v = sw_g(&c, n);
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
@@ -214,8 +219,11 @@ __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
                 }
             }
         }
-        if (live && lo > 0) atomicAdd(&bins[lo], c.w);
+        if (live && lo == th.K) wtop += w;
+        else if (live && lo > 0) atomicAdd(&bins[lo], w);
     }
+    wtop = wave_sum_i32(wtop);
+    if (lane_id() == 0 && wtop != 0) atomicAdd(&bins[th.K], wtop);
     __syncthreads();
     if (threadIdx.x <= th.K && threadIdx.x > 0 && bins[threadIdx.x] != 0)
         atomicAdd((unsigned long long*)(S.red + threadIdx.x), (unsigned long long)bins[threadIdx.x]);
@@ -729,7 +737,11 @@ int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
     th.K = K;
     for (int i = 0; i < K; ++i) th.v[i] = v[i];
     SH_TRY(zero_red(S, K + 1));
-    LAUNCH(S, k_probe<LEVEL>, dim3(nblk((int64_t)S->NL * S->T)), dim3(kTB), 0, S->h->stream, S->dv, th);
+    /* the price probe is bound by its block → global flush (K atomics per
+     * block): a bounded grid; the level probe by its fp64 work: full grid */
+    const unsigned pb = nblk((int64_t)S->NL * S->T);
+    const unsigned grid = (!LEVEL && pb > (unsigned)kProbeBlocks) ? (unsigned)kProbeBlocks : pb;
+    LAUNCH(S, k_probe<LEVEL>, dim3(grid), dim3(kTB), 0, S->h->stream, S->dv, th);
     int64_t bins[SW_SHARD_K + 1];
     SH_TRY(coll_reduce(S, S->dv.red, K + 1, 0, bins));
     int64_t suf = 0;
