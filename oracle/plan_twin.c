@@ -380,10 +380,34 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
     if (N > 0 && P->k > 0.0) {
         double lb = 0.0;
         for (int32_t j = 0; j < N; ++j) lb = sw_max(lb, sw_g(&P->jc[j], P->Tj[j]));
+        /* M_lo = the smallest level whose forced rounds fit, min{M : F(M) ≤ C},
+         * F(M) = Σ_j w_j·#{n < T_j : g_j(n) > M}.  F only steps at the row
+         * values g_j(n), so the answer is one of them (or lb): each probe at
+         * the value midpoint x also returns the largest row value ≤ x and the
+         * smallest > x, and the bracket jumps to those.  Same answer as a
+         * bisection over the fp64 bits of M, in far fewer passes. */
         uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
         while (lo < hi) {
-            uint64_t mid = lo + ((hi - lo) >> 1);
-            if (feasible_level(P, sw_from_bits(mid))) hi = mid; else lo = mid + 1;
+            double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+            if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
+            if (sw_bits(x) < lo) x = sw_from_bits(lo);
+            int64_t F = 0;
+            uint64_t bmax = 0, bmin = UINT64_MAX;
+            for (int32_t j = 0; j < N; ++j) {
+                const int32_t c = lforce(P, j, x);
+                F += (int64_t)P->jc[j].w * c;
+                if (c < P->Tj[j]) {
+                    const uint64_t b = sw_bits(sw_g(&P->jc[j], c));
+                    bmax = b > bmax ? b : bmax;
+                }
+                if (c > 0) {
+                    const uint64_t b = sw_bits(sw_g(&P->jc[j], c - 1));
+                    bmin = b < bmin ? b : bmin;
+                }
+            }
+            P->passes++;
+            if (F <= P->C) hi = bmax >= lo ? bmax : lo;
+            else lo = bmin <= hi ? bmin : hi;
         }
         M_lo = sw_from_bits(lo);
         select_level(P, M_lo, 0, n, l, tk, tmp, &ev, rho_inf, SW_KEY_INF_BITS);

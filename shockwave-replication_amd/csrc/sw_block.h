@@ -22,6 +22,7 @@ struct sw_xchg {
     int64_t i[2][SW_WAVES][2];
     double d[2][SW_WAVES][2];
     uint64_t u[2][SW_WAVES];
+    uint64_t u2[2][SW_WAVES][2];
     int32_t s[2][SW_WAVES];
 };
 
@@ -231,6 +232,32 @@ struct sw_blk {
         for (int w = 1; w < SW_WAVES; ++w) m = X->d[par][w][0] > m ? X->d[par][w][0] : m;
         flip();
         return m;
+    }
+
+    /* Σ v (fits 32 bits per wave), max mx and min mn, one barrier. */
+    __device__ __forceinline__ void sum_max_min(int64_t v, uint64_t mx, uint64_t mn, int64_t& S,
+                                                uint64_t& MX, uint64_t& MN) {
+        const int64_t w = wave_sum_i32((int32_t)v);
+        mx = wave_max(mx);
+        mn = wave_min(mn);
+        if (lane_id() == 0) {
+            X->i[par][wave_id()][0] = w;
+            X->u2[par][wave_id()][0] = mx;
+            X->u2[par][wave_id()][1] = mn;
+        }
+        __syncthreads();
+        int64_t t = 0;
+        uint64_t a = 0, b = ~0ull;
+#pragma unroll
+        for (int k = 0; k < SW_WAVES; ++k) {
+            t += X->i[par][k][0];
+            a = X->u2[par][k][0] > a ? X->u2[par][k][0] : a;
+            b = X->u2[par][k][1] < b ? X->u2[par][k][1] : b;
+        }
+        flip();
+        S = t;
+        MX = a;
+        MN = b;
     }
 
     /* sw_detsum of the per-thread partials v, and the max of m, together. */

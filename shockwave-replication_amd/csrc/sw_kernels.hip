@@ -425,10 +425,32 @@ struct Ctx {
                 double lb = 0.0;
                 for_jobs([&](int j, int s) { lb = sw_max(lb, gval(j, s, Tj(j, s))); });
                 lb = blk.dmax(lb);
+                /* twin: the M_lo search that snaps to row values */
                 uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
                 while (lo < hi) {
-                    const uint64_t mid = lo + ((hi - lo) >> 1);
-                    if (feasible_level(sw_from_bits(mid))) hi = mid; else lo = mid + 1;
+                    double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+                    if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
+                    if (sw_bits(x) < lo) x = sw_from_bits(lo);
+                    int64_t f = 0;
+                    uint64_t bmx = 0, bmn = ~0ull;
+                    for_jobs([&](int j, int s) {
+                        const int cn = lforce(j, s, x);
+                        f += (int64_t)jc(j, s).w * cn;
+                        if (cn < Tj(j, s)) {
+                            const uint64_t b = sw_bits(gval(j, s, cn));
+                            bmx = b > bmx ? b : bmx;
+                        }
+                        if (cn > 0) {
+                            const uint64_t b = sw_bits(gval(j, s, cn - 1));
+                            bmn = b < bmn ? b : bmn;
+                        }
+                    });
+                    int64_t F;
+                    uint64_t BMX, BMN;
+                    blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
+                    passes++;
+                    if (F <= C) hi = BMX >= lo ? BMX : lo;
+                    else lo = BMN <= hi ? BMN : hi;
                 }
                 M_lo = sw_from_bits(lo);
                 plo = rho_inf;
