@@ -58,5 +58,5 @@ struct sw_batch_dev {
     int32_t* planned;
     sw_out_dev* out;
     sw_ws_dev ws;
-    uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][8] cycles */
+    uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][16] cycles (8…13: pack round-loop phases) */
 };

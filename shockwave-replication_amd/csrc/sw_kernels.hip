@@ -42,7 +42,7 @@ namespace {
         __syncthreads();                                                          \
         if (threadIdx.x == 0 && B.stamps) {                                       \
             uint64_t now_ = __builtin_amdgcn_s_memtime();                         \
-            B.stamps[(size_t)blockIdx.x * 8 + (slot)] += now_ - stamp_prev_;      \
+            B.stamps[(size_t)blockIdx.x * 16 + (slot)] += now_ - stamp_prev_;      \
             stamp_prev_ = now_;                                                   \
         }                                                                         \
     } while (0)
@@ -79,6 +79,9 @@ struct Ctx {
     /* inputs (instance-relative) */
     const int32_t* w_in;
     const double* p_in;
+#ifdef SW_STAMPS
+    uint64_t* swp; /* pack phase stamps of this instance */
+#endif
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
     uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
     uint64_t *ycur, *ybest, *y2;
@@ -673,7 +676,12 @@ struct Ctx {
                 const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
                 st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
             }
+            #ifdef SW_STAMPS
+            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp,
+                                   swp);
+#else
             sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp);
+#endif
             for_jobs([&](int j, int s) {
                 (void)s;
                 if (owns(MODE, nin, j)) placed_out[j] = 0;
@@ -866,6 +874,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     const int N = c.N;
     const int64_t jo = I->job_off;
     c.w_in = B.w + jo;
+#ifdef SW_STAMPS
+    c.swp = B.stamps ? B.stamps + (size_t)blockIdx.x * 16 + 8 : nullptr;
+#endif
     c.p_in = B.p + jo;
 
     size_t off = 0;

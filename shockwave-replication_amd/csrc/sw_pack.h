@@ -24,16 +24,15 @@
 #include "sw_block.h"
 
 #ifdef SW_STAMPS
-/* diagnostic builds: cycles per round-loop phase, thread 0's view
- * (0 setup, 1 histogram+need, 2 tiers, 3 fill, 4 tail, 5 apply) */
-__device__ uint64_t g_sw_pack_stamps[8];
-#define SWP_STAMP(k)                                                            \
-    do {                                                                        \
-        if (threadIdx.x == 0) {                                                 \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime();                 \
-            atomicAdd((unsigned long long*)&g_sw_pack_stamps[k], now_ - swp_t_); \
-            swp_t_ = now_;                                                      \
-        }                                                                       \
+/* diagnostic builds: cycles per round-loop phase, thread 0's view, added
+ * to swp[k] (0 setup, 1 histogram+need, 2 tiers, 3 fill, 4 tail, 5 apply) */
+#define SWP_STAMP(k)                                         \
+    do {                                                     \
+        if (threadIdx.x == 0 && swp) {                       \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+            swp[k] += now_ - swp_t_;                         \
+            swp_t_ = now_;                                   \
+        }                                                    \
     } while (0)
 #else
 #define SWP_STAMP(k) \
@@ -88,7 +87,9 @@ __device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int 
 template <int E>
 __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int A, int T, int G,
                                                uint32_t (&st)[E], uint64_t (&mk)[E],
-                                               const int32_t* caps = nullptr) {
+                                               const int32_t* caps = nullptr,
+                                               uint64_t* swp = nullptr) {
+    (void)swp; /* phase stamps (SW_STAMPS builds) */
     const int tid = threadIdx.x;
     const int lane = lane_id();
 #ifdef SW_STAMPS

@@ -51,6 +51,11 @@
 #include "sw_shard_ctl.h"
 #include "sw_validate.h"
 
+#ifdef SW_STAMPS
+/* diagnostic builds: k_pack_rounds phase cycles (sw_pack.h SWP_STAMP) */
+__device__ uint64_t g_sw_pack_stamps[8];
+#endif
+
 namespace {
 
 constexpr int kTB = 256;  /* threads per block of the per-job kernels */
@@ -536,7 +541,11 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
         st[i] = E * tid + i < A ? v : 0u;
         ent[i] = E * tid + i < A ? ent[i] : -1;
     }
+    #ifdef SW_STAMPS
+    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr, g_sw_pack_stamps);
+#else
     sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr);
+#endif
 #pragma unroll
     for (int i = 0; i < E; ++i) {
         if (ent[i] < 0) continue;

@@ -32,17 +32,23 @@ def main():
         s.upload(batch)
         s.run()
         res = s.download()
-        st = np.zeros(len(batch) * 8, dtype=np.uint64)
+        st = np.zeros(len(batch) * 16, dtype=np.uint64)
         lib.sw_debug_stamps(s.h, st.ctypes.data_as(C.POINTER(C.c_uint64)))
-        st = st.reshape(len(batch), 8)[:, :6].astype(np.float64)
+        st = st.reshape(len(batch), 16).astype(np.float64)
+        pk = st[:, 8:14]
+        st = st[:, :6]
         tot = st.sum(axis=1).mean()
         print(f"{name}: mean cycles/instance {tot:.0f}; passes {np.mean([r['iters'] for r in res]):.1f}; "
               f"status {sorted(set(r['status'] for r in res))}")
         for i, n in enumerate(names):
             print(f"   {n:16s} {st[:, i].mean():12.0f}  {100 * st[:, i].mean() / tot:5.1f}%")
+        pnames = ["setup", "hist+need", "tiers", "fill", "tail", "apply"]
+        print("   pack round loop (all packs of an instance):",
+              " ".join(f"{n} {pk[:, i].mean():.0f}" for i, n in enumerate(pnames)))
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
-            for r, row in list(zip(res, st))[:24]:
-                print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row))
+            for r, row, prow in list(zip(res, st, pk))[:24]:
+                print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row), "|",
+                      " ".join(f"{v:8.0f}" for v in prow))
         s.close()
 
 
