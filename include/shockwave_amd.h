@@ -204,6 +204,16 @@ int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset
                        int64_t total_jobs, sw_result* res);
 int sw_dist_shard_range(int64_t total_jobs, int32_t world, int32_t rank, int64_t* lo,
                         int64_t* hi);
+/*
+ * Device-resident variant ("host (or device) pointers"):
+ * local's per-job arrays are device pointers on the handle's device, and
+ * res->plan / res->planned_rounds are device pointers (or NULL), written on
+ * the handle's stream — nothing crosses PCIe but the step scalars.  The
+ * per-job checks of the host path run on the device; a bad input on any rank
+ * returns SW_ERR_INVALID on every rank.  Synchronous like sw_dist_plan_solve.
+ */
+int sw_dist_plan_solve_dev(sw_handle* h, const sw_problem* local, int64_t job_offset,
+                           int64_t total_jobs, sw_result* res);
 
 /*
  * Host collectives (blocking, in rank order, same call sequence on every

@@ -449,6 +449,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.pack = e_pack;
     ops.class_caps = e_class_caps;
     ops.pack_class = e_pack_class;
+    ops.search = NULL; /* the controller's own K-ary loop */
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,
                             &res->status);

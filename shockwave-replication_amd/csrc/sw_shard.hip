@@ -139,15 +139,24 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
                                                const double* d, const int32_t* F,
                                                const int32_t* E, const double* R, double delta) {
     const int i = blockIdx.x * kTB + threadIdx.x;
-    uint64_t amax = 0, lb = 0;
+    uint64_t amax = 0, lb = 0, bad = 0;
     if (i < S.NL) {
-        const sw_jobc c = sw_make_jobc((int32_t)S.N, S.T, delta, w[i], d[i], F[i], E[i], R[i], S.p[i]);
-        jc[i] = c;
-        amax = sw_bits(c.a); /* a, g ≥ 0: bit order = value order */
-        lb = sw_bits(sw_g(&c, tj_of(S, c)));
+        /* the per-job checks of sw_validate_problem, on the device: device-
+         * resident inputs (sw_dist_plan_solve_dev) never visit the host */
+        const double pj = S.p[i];
+        bad = w[i] < 1 || E[i] < 1 || F[i] < 0 || F[i] > E[i] || (w[i] <= S.G && w[i] > SW_MAX_WIDTH) ||
+              !(d[i] > 0.0) || !(d[i] < 1e308) || !(R[i] == R[i] && R[i] < 1e308 && R[i] > -1e308) ||
+              !(pj >= 0.0) || !(pj < 1e308);
+        if (!bad) {
+            const sw_jobc c = sw_make_jobc((int32_t)S.N, S.T, delta, w[i], d[i], F[i], E[i], R[i], pj);
+            jc[i] = c;
+            amax = sw_bits(c.a); /* a, g ≥ 0: bit order = value order */
+            lb = sw_bits(sw_g(&c, tj_of(S, c)));
+        }
     }
     red_umax(S.red + 0, amax);
     red_umax(S.red + 1, lb);
+    red_umax(S.red + 2, bad);
 }
 
 /* key rows (twin: build), A read from the all-reduced step result */
@@ -186,14 +195,10 @@ __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf)
 
 /* K probes at once: item (job, n) adds w to bin #{m : thr_m < v(n)} (v =
  * the key, or g for the level probes); the count for probe m is the suffix
- * Σ_{b > m} bin[b] (host side).  Thread per item: the whole grid is busy. */
+ * Σ_{b > m} bin[b].  Thread per item: the whole grid is busy. */
 template <bool LEVEL>
-__global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
-    __shared__ int32_t bins[SW_SHARD_K + 1];
-    __shared__ uint64_t thr[SW_SHARD_K];
-    if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
-    if (threadIdx.x < th.K) thr[threadIdx.x] = th.v[threadIdx.x];
-    __syncthreads();
+__device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* thr, int K,
+                                           int32_t* bins) {
     /* grid-stride over the items (NL·T < 2^31): a bounded grid keeps the
      * block → global flush at ≤ kProbeBlocks·K atomics per probe */
     const int items = S.NL * S.T;
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
         const int32_t w = S.jc[i].w;
         const int tj = w <= S.G ? S.T : 0;
         bool live;
-        int lo = 0, hi = th.K;
+        int lo = 0, hi = K;
         if (LEVEL) {
             live = n < tj;
             if (live) {
@@ -224,14 +229,98 @@ __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
                 }
             }
         }
-        if (live && lo == th.K) wtop += w;
+        if (live && lo == K) wtop += w;
         else if (live && lo > 0) atomicAdd(&bins[lo], w);
     }
     wtop = wave_sum_i32(wtop);
-    if (lane_id() == 0 && wtop != 0) atomicAdd(&bins[th.K], wtop);
+    if (lane_id() == 0 && wtop != 0) atomicAdd(&bins[K], wtop);
     __syncthreads();
-    if (threadIdx.x <= th.K && threadIdx.x > 0 && bins[threadIdx.x] != 0)
+    if (threadIdx.x <= K && threadIdx.x > 0 && bins[threadIdx.x] != 0)
         atomicAdd((unsigned long long*)(S.red + threadIdx.x), (unsigned long long)bins[threadIdx.x]);
+}
+
+/* thresholds given by the host (controller-driven search step) */
+template <bool LEVEL>
+__global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
+    __shared__ int32_t bins[SW_SHARD_K + 1];
+    __shared__ uint64_t thr[SW_SHARD_K];
+    if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
+    if (threadIdx.x < th.K) thr[threadIdx.x] = th.v[threadIdx.x];
+    __syncthreads();
+    probe_body<LEVEL>(S, thr, th.K, bins);
+}
+
+/* ---- device-chained K-ary search (op_search) ---------------------------------
+ * The controller's swc_search loop (sw_shard_ctl.h) with its state in device
+ * memory: sr[0] = lo, sr[1] = hi, sr[2] = budget (i64), sr[3] = rounds taken.
+ * Each round is k_probe_dev → (RCCL all-reduce of the bins) → k_search_update
+ * on the stream, with no host round trip; a round whose bracket is already
+ * closed does nothing, so the host enqueues the worst-case round count. */
+struct SearchPts {
+    int32_t K;
+    uint64_t a, b, d;
+};
+__device__ __forceinline__ SearchPts search_pts(uint64_t lo, uint64_t hi) {
+    SearchPts q;
+    const uint64_t span = hi - lo;
+    q.K = lo >= hi ? 0 : (span < (uint64_t)SW_SHARD_K ? (int32_t)span : SW_SHARD_K);
+    q.d = (uint64_t)q.K + 1u;
+    q.a = lo >= hi ? 0 : span / q.d;
+    q.b = lo >= hi ? 0 : span % q.d;
+    return q;
+}
+__device__ __forceinline__ uint64_t search_pt(uint64_t lo, const SearchPts& q, int i) {
+    const uint64_t m = (uint64_t)(i + 1);
+    return lo + q.a * m + (q.b * m) / q.d;
+}
+
+__global__ void k_search_init(unsigned long long* sr, unsigned long long lo, unsigned long long hi,
+                              long long bud) {
+    if (threadIdx.x == 0) { sr[0] = lo; sr[1] = hi; sr[2] = (unsigned long long)bud; sr[3] = 0; }
+}
+
+template <bool LEVEL>
+__global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned long long* sr) {
+    __shared__ int32_t bins[SW_SHARD_K + 1];
+    __shared__ uint64_t thr[SW_SHARD_K];
+    const uint64_t lo = sr[0], hi = sr[1];
+    const SearchPts q = search_pts(lo, hi);
+    if (q.K == 0) return; /* bracket closed: uniform over the grid */
+    if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
+    if ((int)threadIdx.x < q.K) {
+        const uint64_t v = search_pt(lo, q, (int)threadIdx.x);
+        thr[threadIdx.x] = LEVEL ? v : (uint64_t)(uint32_t)v; /* price bits are u32 */
+    }
+    __syncthreads();
+    probe_body<LEVEL>(S, thr, q.K, bins);
+}
+
+/* counts cnt[i] = Σ_{b > i} bins[b]; the first i with cnt ≤ budget closes
+ * the bracket (swc_search).  One wave: lane i loads bins[i + 1], a shuffle
+ * suffix scan forms cnt[i], a ballot finds the first i. */
+__global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, const long long* bins) {
+    const uint64_t lo = sr[0], hi = sr[1];
+    const int64_t bud = (int64_t)sr[2];
+    const SearchPts q = search_pts(lo, hi);
+    if (q.K == 0) return;
+    const int i = (int)threadIdx.x;
+    int64_t cnt = (i < q.K) ? (int64_t)bins[i + 1] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t v = __shfl_down(cnt, o, 64);
+        cnt += (i + o < 64) ? v : 0;
+    }
+    const uint64_t ok = __ballot(i < q.K && cnt <= bud);
+    if (i == 0) {
+        if (ok) {
+            const int f = __builtin_ctzll(ok);
+            sr[1] = search_pt(lo, q, f);
+            if (f > 0) sr[0] = search_pt(lo, q, f - 1) + 1u;
+        } else {
+            sr[0] = search_pt(lo, q, q.K - 1) + 1u;
+        }
+        sr[3] += 1;
+    }
 }
 
 __global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b) {
@@ -585,6 +674,11 @@ struct sw_shard_state {
     DevBuf<long long> red;
     DevBuf<sw_pack_ent> psend, pall;
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
+    DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
+    /* this solve's per-job inputs on the device: the buffers above after an
+     * upload, or the caller's own HBM (sw_dist_plan_solve_dev) */
+    const int32_t *in_w = nullptr, *in_F = nullptr, *in_E = nullptr;
+    const double *in_d = nullptr, *in_R = nullptr, *in_p = nullptr;
     int ring_pos = kRing; /* next step-result slice (kRing = clear the ring first) */
     bool zero_pending = false;
     /* pinned staging */
@@ -709,11 +803,12 @@ int zero_red(sw_shard_state* S, int n) {
 int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
-    SH_TRY(zero_red(S, 2));
-    LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->w.p, S->d.p, S->F.p,
-           S->E.p, S->R.p, S->delta);
-    uint64_t mx[2];
-    SH_TRY(coll_reduce(S, S->dv.red, 2, 1, mx));
+    SH_TRY(zero_red(S, 3));
+    LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->in_w, S->in_d, S->in_F,
+           S->in_E, S->in_R, S->delta);
+    uint64_t mx[3];
+    SH_TRY(coll_reduce(S, S->dv.red, 3, 1, mx));
+    if (mx[2]) return S->h->err = "invalid problem (per-job inputs)", SW_ERR_INVALID; /* every rank */
     if (S->host_comm && S->world > 1) { /* kernels read A from red[0] */
         memcpy(S->hx.p, mx, 16);
         SH_HIP(S, hipMemcpyAsync(S->dv.red, S->hx.p, 16, hipMemcpyHostToDevice, st));
@@ -726,7 +821,7 @@ int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
     int32_t* wsend = (int32_t*)S->xsend.p;
     int32_t* wrecv = (int32_t*)S->xrecv.p;
     SH_HIP(S, hipMemsetAsync(wsend, 0, (size_t)S->P * 4, st));
-    if (S->NL) SH_HIP(S, hipMemcpyAsync(wsend, S->w.p, (size_t)S->NL * 4, hipMemcpyDeviceToDevice, st));
+    if (S->NL) SH_HIP(S, hipMemcpyAsync(wsend, S->in_w, (size_t)S->NL * 4, hipMemcpyDeviceToDevice, st));
     S->w_all.resize((size_t)S->P * S->world);
     SH_TRY(coll_gather(S, wsend, wrecv, (size_t)S->P * 4, S->w_all.data()));
     for (int64_t j = 0; j < S->N; ++j) w_all[j] = S->w_all[j]; /* rank r's block starts at job r·P */
@@ -768,6 +863,46 @@ int op_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
     uint64_t v[SW_SHARD_K];
     for (int i = 0; i < K; ++i) v[i] = sw_bits(M[i]);
     return probe<true>((sw_shard_state*)ctx, v, K, out);
+}
+
+/* swc_search with every round on the stream: probe → (all-reduce) → update,
+ * the worst-case number of rounds enqueued (closed rounds are no-ops), one
+ * read-back at the end.  RCCL or a single rank only: host collectives need
+ * the host between rounds and use the controller's loop. */
+int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
+              int32_t* rounds) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    /* each round leaves a span ≤ ⌊span / 64⌋, so the rounds are at most the
+     * base-64 digits of the initial span */
+    int nr = 0;
+    for (uint64_t sp = lo < hi ? hi - lo : 0; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nr;
+    *rounds = 0;
+    *out = lo;
+    if (nr == 0) return SW_OK;
+    unsigned long long* sr = S->srch.p;
+    LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sr, (unsigned long long)lo,
+           (unsigned long long)hi, (long long)bud);
+    const unsigned pb = nblk((int64_t)S->NL * S->T);
+    for (int r = 0; r < nr; ++r) {
+        SH_TRY(zero_red(S, SW_SHARD_K + 1));
+        if (kind == 0)
+            LAUNCH(S, k_probe_dev<false>, dim3(pb > (unsigned)kProbeBlocks ? (unsigned)kProbeBlocks : pb),
+                   dim3(kTB), 0, st, S->dv, sr);
+        else
+            LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, sr);
+        if (S->comm && S->world > 1)
+            SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
+                                     S->comm, st));
+        LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, S->dv.red);
+    }
+    SH_HIP(S, hipMemcpyAsync(S->hx.p, sr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipStreamSynchronize(st));
+    unsigned long long v[4];
+    memcpy(v, S->hx.p, sizeof(v));
+    *out = v[0];
+    *rounds = (int32_t)v[3];
+    return SW_OK;
 }
 
 int op_between(void* ctx, double a, double b, int64_t* out) {
@@ -927,7 +1062,8 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* cap
 }
 
 /* Reserve the per-solve buffers and upload this rank's jobs. */
-int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
+int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, bool dev,
+            const sw_result* res) {
     hipStream_t st = S->h->stream;
     S->NL = pr->num_jobs;
     S->T = pr->future_rounds;
@@ -948,12 +1084,21 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
                S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
-               S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64);
+               S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64) ||
+               S->srch.reserve(4);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
     if (bad || S->hx.reserve(std::max<size_t>(xbytes * S->world, kRed * 8)))
         return S->h->err = "shard allocation failed", SW_ERR_HIP;
-    if (S->NL) {
+    if (dev) {
+        S->in_w = pr->nworkers; S->in_F = pr->completed_epochs; S->in_E = pr->total_epochs;
+        S->in_d = pr->epoch_duration; S->in_R = pr->remaining_runtime; S->in_p = pr->priority;
+        S->zero_pending = S->NL > 0;
+    } else {
+        S->in_w = S->w.p; S->in_F = S->F.p; S->in_E = S->E.p;
+        S->in_d = S->d.p; S->in_R = S->R.p; S->in_p = S->p.p;
+    }
+    if (S->NL && !dev) {
         const size_t n = (size_t)S->NL;
         SH_HIP(S, hipMemcpyAsync(S->w.p, pr->nworkers, n * 4, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipMemcpyAsync(S->F.p, pr->completed_epochs, n * 4, hipMemcpyHostToDevice, st));
@@ -973,11 +1118,13 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N) {
         v.beta[b] = b < pr->num_bases ? pr->bases[b] : 0.0;
         v.ell[b] = b < pr->num_bases ? pr->log_bases[b] : 0.0;
     }
-    v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->p.p; v.l = S->l.p; v.taken = S->taken.p;
+    v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->in_p; v.l = S->l.p; v.taken = S->taken.p;
     v.tie = S->tie.p; v.xa = S->xa.p;
     for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
     for (int a = 0; a < SW_Y_COUNT; ++a) v.y[a] = S->y[a].p;
     v.plan = S->plan.p; v.planned = S->planned.p; v.red = S->red.p;
+    if (dev && res->plan) v.plan = res->plan; /* the final step writes the caller's HBM */
+    if (dev && res->planned_rounds) v.planned = res->planned_rounds;
     S->ring_pos = kRing; /* the first step clears the ring */
     if (S->zero_pending) {
         LAUNCH(S, k_zero_state, dim3(nblk(S->NL)), dim3(kTB), 0, st, v);
@@ -1011,7 +1158,7 @@ void sw_shard_release(sw_handle* h) {
     S->planned.release(); S->prank.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
-    S->caps.release(); S->hcaps.release();
+    S->caps.release(); S->hcaps.release(); S->srch.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
@@ -1073,18 +1220,31 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
     return SW_OK;
 }
 
-int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
-                       sw_result* res) {
-    if (!h || !res) return SW_ERR_INVALID;
+}  // extern "C"
+
+namespace {
+int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
+               sw_result* res, bool dev) {
+    if (!h || !res || !local) return SW_ERR_INVALID;
     if (!h->shard) return h->err = "sw_dist_init / sw_dist_init_host first", SW_ERR_INVALID;
     sw_shard_state* S = h->shard;
-    if (sw_validate_problem(local) != 0) return h->err = "invalid problem", SW_ERR_INVALID;
+    if (dev) { /* scalars here; the per-job checks run in k_setup */
+        sw_problem sc = *local;
+        sc.num_jobs = 0;
+        if (sw_validate_problem(&sc) != 0 || local->num_jobs < 0 ||
+            (local->num_jobs > 0 && (!local->nworkers || !local->epoch_duration ||
+                                     !local->completed_epochs || !local->total_epochs ||
+                                     !local->remaining_runtime || !local->priority)))
+            return h->err = "invalid problem", SW_ERR_INVALID;
+    } else if (sw_validate_problem(local) != 0) {
+        return h->err = "invalid problem", SW_ERR_INVALID;
+    }
     int64_t lo, hi;
     if (sw_shard_range(total_jobs, S->world, S->rank, &lo, &hi) != 0 || lo != job_offset ||
         hi - lo != local->num_jobs)
         return h->err = "slice does not match sw_dist_shard_range", SW_ERR_INVALID;
     if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
-    SH_TRY(prepare(S, local, job_offset, total_jobs));
+    SH_TRY(prepare(S, local, job_offset, total_jobs, dev, res));
     sw_shard_ops ops;
     ops.ctx = S;
     ops.setup = op_setup;
@@ -1103,12 +1263,13 @@ int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset
     ops.pack = op_pack;
     ops.class_caps = op_class_caps;
     ops.pack_class = op_pack_class;
+    ops.search = S->host_comm ? nullptr : op_search;
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,
                             &res->p2_objective, &res->bound, &res->iters, &res->status);
     if (rc < 0) return rc == -1 ? (h->err = "out of host memory", SW_ERR_HIP) : rc;
     const size_t n = (size_t)S->NL;
-    if (n) {
+    if (n && !dev) {
         if (res->plan)
             SH_HIP(S, hipMemcpyAsync(res->plan, S->plan.p, n * S->T, hipMemcpyDeviceToHost, h->stream));
         if (res->planned_rounds)
@@ -1117,6 +1278,19 @@ int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset
     }
     SH_HIP(S, hipStreamSynchronize(h->stream));
     return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
+                       sw_result* res) {
+    return dist_solve(h, local, job_offset, total_jobs, res, false);
+}
+
+int sw_dist_plan_solve_dev(sw_handle* h, const sw_problem* local, int64_t job_offset,
+                           int64_t total_jobs, sw_result* res) {
+    return dist_solve(h, local, job_offset, total_jobs, res, true);
 }
 
 }  // extern "C"

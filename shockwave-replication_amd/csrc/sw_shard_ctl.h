@@ -111,6 +111,12 @@ typedef struct sw_shard_ops {
      * and leaves every other job untouched */
     int (*pack_class)(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
                       int32_t pdst);
+    /* optional (NULL = the controller drives count_gt / feasible itself):
+     * the whole K-ary search of swc_search inside the engine — kind 0 over
+     * count_gt, 1 over feasible — returning its answer and the number of
+     * rounds (collective steps) it took, which must equal swc_search's */
+    int (*search)(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
+                  int32_t* rounds);
 } sw_shard_ops;
 
 /* Job range of `rank` (sw_dist_shard_range in include/shockwave_amd.h). */
@@ -176,6 +182,12 @@ static inline int swc_search(sw_shard_ctl* c, int kind, uint64_t lo, uint64_t hi
     uint32_t rho[SW_SHARD_K];
     double Ms[SW_SHARD_K];
     int64_t cnt[SW_SHARD_K];
+    if (c->ops->search) {
+        int32_t rounds = 0;
+        SWC_TRY(c->ops->search(c->ops->ctx, kind, lo, hi, bud, out, &rounds));
+        c->steps += rounds;
+        return 0;
+    }
     while (lo < hi) {
         const uint64_t span = hi - lo;
         const int32_t K = span < (uint64_t)SW_SHARD_K ? (int32_t)span : SW_SHARD_K;

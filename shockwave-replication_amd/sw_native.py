@@ -246,6 +246,42 @@ class ProblemArrays:
         return r
 
 
+class DeviceShard:
+    """One rank's jobs resident in HBM (torch tensors on `device`) for
+    sw_dist_plan_solve_dev; plan [N, T] u8 and planned_rounds [N] i32 are
+    device tensors the solve writes."""
+
+    def __init__(self, arrays: ProblemArrays, device):
+        import torch
+        self.a = arrays
+        dev = torch.device(device)
+        self.w = torch.from_numpy(arrays.w).to(dev)
+        self.d = torch.from_numpy(arrays.d).to(dev)
+        self.F = torch.from_numpy(arrays.F).to(dev)
+        self.E = torch.from_numpy(arrays.E).to(dev)
+        self.R = torch.from_numpy(arrays.R).to(dev)
+        self.p = torch.from_numpy(arrays.p).to(dev)
+        self.plan = torch.zeros((arrays.N, arrays.T), dtype=torch.uint8, device=dev)
+        self.planned = torch.zeros(arrays.N, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)  # the handle's stream does not order after torch's
+
+    def c_problem(self) -> SwProblem:
+        p = self.a.c_problem()  # scalars and the host bases table
+        p.nworkers = C.cast(C.c_void_p(self.w.data_ptr()), _ip)
+        p.epoch_duration = C.cast(C.c_void_p(self.d.data_ptr()), _dp)
+        p.completed_epochs = C.cast(C.c_void_p(self.F.data_ptr()), _ip)
+        p.total_epochs = C.cast(C.c_void_p(self.E.data_ptr()), _ip)
+        p.remaining_runtime = C.cast(C.c_void_p(self.R.data_ptr()), _dp)
+        p.priority = C.cast(C.c_void_p(self.p.data_ptr()), _dp)
+        return p
+
+    def c_result(self) -> SwResult:
+        r = SwResult()
+        r.plan = C.cast(C.c_void_p(self.plan.data_ptr()), _up)
+        r.planned_rounds = C.cast(C.c_void_p(self.planned.data_ptr()), _ip)
+        return r
+
+
 def result_dict(r: SwResult, arrays: ProblemArrays, rc: int) -> dict:
     return {
         "rc": rc,
@@ -276,7 +312,7 @@ EXPORTED_SYMBOLS = (
     "sw_plan_solve", "sw_plan_solve_batch", "sw_batch_upload", "sw_batch_run",
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
     "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
-    "sw_dist_init_host", "sw_mmf_allocate",
+    "sw_dist_init_host", "sw_mmf_allocate", "sw_dist_plan_solve_dev",
 )
 
 
@@ -331,6 +367,9 @@ def load(path: str | None = None):
     lib.sw_dist_plan_solve.argtypes = [C.c_void_p, C.POINTER(SwProblem), C.c_int64, C.c_int64,
                                        C.POINTER(SwResult)]
     lib.sw_dist_plan_solve.restype = C.c_int
+    lib.sw_dist_plan_solve_dev.argtypes = [C.c_void_p, C.POINTER(SwProblem), C.c_int64, C.c_int64,
+                                           C.POINTER(SwResult)]
+    lib.sw_dist_plan_solve_dev.restype = C.c_int
     lib.sw_dist_shard_range.argtypes = [C.c_int64, C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     lib.sw_dist_shard_range.restype = C.c_int
@@ -454,6 +493,17 @@ class Solver:
             raise NativeError(f"sw_dist_plan_solve: collective failed: {comm.error!r}")
         self._check(rc, "sw_dist_plan_solve")
         return result_dict(res, local, rc)
+
+    def dist_solve_dev(self, shard: "DeviceShard", job_offset: int, total_jobs: int) -> dict:
+        """sw_dist_plan_solve_dev: inputs and the plan stay in HBM (shard's
+        tensors); only the scalar results come back."""
+        prob, res = shard.c_problem(), shard.c_result()
+        rc = self.lib.sw_dist_plan_solve_dev(self.h, C.byref(prob), int(job_offset),
+                                             int(total_jobs), C.byref(res))
+        self._check(rc, "sw_dist_plan_solve_dev")
+        return {"rc": rc, "objective": res.objective, "utility": res.utility,
+                "makespan": res.makespan, "p2_objective": res.p2_objective, "bound": res.bound,
+                "iters": res.iters, "status": res.status}
 
 
 class MmfAllocator:

@@ -93,3 +93,35 @@ def test_gpu_shard_rejects_bad_slice(rccl_solver):
     a = ss.synth_problem(0, 100, 32, 10, 120.0, 1e5, 5.0)
     with pytest.raises(sn.NativeError):
         rccl_solver.dist_solve(a.slice(0, 50), 0, a.N)
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[6], CASES[7]], ids=["N50", "N900", "N1500"])
+def test_gpu_shard_device_resident(case, rccl_solver):
+    """sw_dist_plan_solve_dev (inputs and plan in HBM) returns exactly what the
+    host-buffer entry point returns: plan bytes, counts, objective bits, steps."""
+    import torch
+    seed, N, G, T, k, lam = case
+    a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+    shard = sn.DeviceShard(a, "cuda:0")
+    torch.cuda.synchronize()
+    rd = rccl_solver.dist_solve_dev(shard, 0, a.N)
+    rh = rccl_solver.dist_solve(a, 0, a.N)
+    assert np.array_equal(shard.plan.cpu().numpy(), rh["plan"])
+    assert np.array_equal(shard.planned.cpu().numpy(), rh["planned_rounds"])
+    for key in ("objective", "utility", "makespan", "p2_objective", "bound", "iters", "status", "rc"):
+        assert rd[key] == rh[key] or (rd[key] != rd[key] and rh[key] != rh[key]), key
+
+
+def test_gpu_shard_device_rejects_bad_input(rccl_solver):
+    """The per-job checks run on the device for HBM-resident inputs."""
+    import torch
+    a = ss.synth_problem(3, 200, 32, 10, 120.0, 1e5, 5.0)
+    shard = sn.DeviceShard(a, "cuda:0")
+    shard.F[7] = shard.E[7] + 1  # completed epochs > total epochs
+    torch.cuda.synchronize()
+    with pytest.raises(sn.NativeError):
+        rccl_solver.dist_solve_dev(shard, 0, a.N)
+    shard.F[7] = 0
+    torch.cuda.synchronize()
+    r = rccl_solver.dist_solve_dev(shard, 0, a.N)  # the handle recovers
+    assert r["rc"] in (0, 1)
