@@ -293,13 +293,48 @@ struct Ctx {
             wgt_star = Wall;
         } else {
             uint32_t lo = plo, hi = phi;
-            while (lo < hi) {
-                const uint32_t mid = lo + ((hi - lo) >> 1);
-                int32_t wg = 0;
-                for_jobs([&](int j, int s) { wg += jc(j, s).w * cnt<false>(j, s, mid, lcur[j]); });
-                wg = blk.sum32(wg);
-                passes++;
-                if (wg <= bud) hi = mid; else lo = mid + 1;
+            if constexpr (ONE) {
+                /* Per-job windows: ca = #keys ≥ lo (= count above lo − 1),
+                 * cb = #keys > hi.  Every probe mid ∈ [lo, hi) counts
+                 * between them, so a job whose window is closed (ca == cb)
+                 * skips its 32 compares; as the bracket narrows, whole
+                 * waves skip.  Same probes, same ρ*. */
+                int ca[SW_JPT], cb[SW_JPT], cm[SW_JPT];
+#pragma unroll
+                for (int s = 0; s < SW_JPT; ++s) { ca[s] = 0; cb[s] = 0; cm[s] = 0; }
+                if (lo < hi)
+                    for_jobs([&](int j, int s) {
+                        ca[s] = cnt<true>(j, s, lo, lcur[j]);
+                        cb[s] = cnt<false>(j, s, hi, lcur[j]);
+                    });
+                while (lo < hi) {
+                    const uint32_t mid = lo + ((hi - lo) >> 1);
+                    int32_t wg = 0;
+                    for_jobs([&](int j, int s) {
+                        int c = cb[s];
+                        if (ca[s] != cb[s]) c = cnt<false>(j, s, mid, lcur[j]);
+                        cm[s] = c;
+                        wg += jc(j, s).w * c;
+                    });
+                    wg = blk.sum32(wg);
+                    passes++;
+                    const bool down = wg <= bud;
+#pragma unroll
+                    for (int s = 0; s < SW_JPT; ++s) {
+                        cb[s] = down ? cm[s] : cb[s];
+                        ca[s] = down ? ca[s] : cm[s];
+                    }
+                    if (down) hi = mid; else lo = mid + 1;
+                }
+            } else {
+                while (lo < hi) {
+                    const uint32_t mid = lo + ((hi - lo) >> 1);
+                    int32_t wg = 0;
+                    for_jobs([&](int j, int s) { wg += jc(j, s).w * cnt<false>(j, s, mid, lcur[j]); });
+                    wg = blk.sum32(wg);
+                    passes++;
+                    if (wg <= bud) hi = mid; else lo = mid + 1;
+                }
             }
             const uint32_t rho = lo;
             ev.rho = rho;

@@ -17,7 +17,8 @@
  *   jc[NL] (sw_jobc, 64 B)   keys[NL][T] fp32   l, taken, 5 count arrays [NL] i32
  *   3 round-bitmask arrays [NL] u64   plan[NL][T] u8   planned[NL] i32
  *   red[128] i64 (step results)   exchange blocks for the gathers
- *   placement: send[P] / all[W·P] entries (24 B), rank[W·P], order[W·P]
+ *   placement: send[P] / all[W·P] entries (24 B), chunk-sorted keys and
+ *   entries [W·P rounded up to 1024], order[W·P]
  *
  * Kernels and what bounds them (all latency-bound at C4's 1,250 jobs per
  * rank; DESIGN.md §7 has the per-step budget):
@@ -31,7 +32,10 @@
  *        workgroup sums each deterministic-sum lane left to right (sw_detsum's
  *        chunks), so the gathered lanes reproduce the single-instance sums
  *        bit for bit
- *   k_pack_rank / k_pack_rounds   the placement (sw_pack.h)
+ *   k_pack_chunk_sort / k_pack_merge_rank   the global placement order: LDS
+ *        bitonic sort per 1024-entry chunk, ranks by binary searches in the
+ *        other sorted chunks
+ *   k_pack_rounds   the round loop of the placement (sw_pack.h)
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -547,54 +551,75 @@ __global__ __launch_bounds__(kTB) void k_zero_state(ShardDev S) {
     S.taken[i] = 0;
 }
 
-/* all-pairs rank: rank[e] += #{active e' in this block's tile : key(e') >
- * key(e)}.  Keys are unique (they end in ~job), so the ranks of the active
- * entries are a permutation of [0, A).  A block ranks kRankPer·kTB entries
- * against a kRankTile tile held in LDS as 16-B (khi, klo) pairs: one
- * ds_read_b128 feeds kRankPer compares. */
-constexpr int kRankTile = 1024;
-constexpr int kRankPer = 4;
 struct alignas(16) key2 {
     uint64_t h, l;
 };
-__global__ __launch_bounds__(kTB) void k_pack_rank(const sw_pack_ent* all, int64_t M, int32_t* rank) {
-    __shared__ key2 tile[kRankTile];
-    const int64_t t0 = (int64_t)blockIdx.y * kRankTile;
-    for (int x = threadIdx.x; x < kRankTile; x += kTB) {
-        const int64_t e = t0 + x;
-        key2 k;
-        k.h = 0; k.l = 0; /* inactive: (0,0) never exceeds an active key */
-        if (e < M && all[e].st != 0) { k.h = all[e].khi; k.l = all[e].klo; }
-        tile[x] = k;
+
+/* Global placement order of the gathered entries, by sorting: each
+ * kSortChunk-entry chunk is bitonic-sorted in LDS (descending; inactive
+ * entries as (0, 0), which every active key exceeds, sort last), then each
+ * active entry's global rank is its chunk position plus, for every other
+ * chunk, the number of its keys above the entry's key (a binary search in
+ * that sorted chunk).  Keys are unique, so the ranks of the active entries
+ * are a permutation of [0, A); order[rank] = entry. */
+constexpr int kSortChunk = 1024;
+constexpr int kSortThreads = kSortChunk / 2;
+__device__ __forceinline__ bool key_gt(const key2& a, const key2& b) {
+    return a.h > b.h || (a.h == b.h && a.l > b.l);
+}
+__global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_ent* all, int64_t M,
+                                                                   key2* skeys, int32_t* sidx) {
+    __shared__ key2 k[kSortChunk];
+    __shared__ int32_t ix[kSortChunk];
+    const int64_t c0 = (int64_t)blockIdx.x * kSortChunk;
+    for (int x = threadIdx.x; x < kSortChunk; x += kSortThreads) {
+        const int64_t e = c0 + x;
+        key2 v;
+        v.h = 0; v.l = 0;
+        if (e < M && all[e].st != 0) { v.h = all[e].khi; v.l = all[e].klo; }
+        k[x] = v;
+        ix[x] = (int32_t)e;
     }
     __syncthreads();
-    uint64_t h[kRankPer], l[kRankPer];
-    int c[kRankPer];
-    bool act[kRankPer];
-    const int64_t e0 = (int64_t)blockIdx.x * kTB * kRankPer + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kRankPer; ++k) {
-        const int64_t e = e0 + (int64_t)k * kTB;
-        act[k] = e < M && all[e].st != 0;
-        h[k] = act[k] ? all[e].khi : ~0ull;
-        l[k] = act[k] ? all[e].klo : ~0ull;
-        c[k] = 0;
+    const int t = threadIdx.x; /* one compare-exchange pair per thread and stage */
+    for (int kk = 2; kk <= kSortChunk; kk <<= 1) {
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            const int i = 2 * t - (t & (jj - 1)); /* bit jj of i is clear */
+            const int q = i + jj;
+            const bool desc = (i & kk) == 0;
+            const key2 a = k[i], b = k[q];
+            if (desc ? key_gt(b, a) : key_gt(a, b)) {
+                k[i] = b; k[q] = a;
+                const int32_t ti = ix[i]; ix[i] = ix[q]; ix[q] = ti;
+            }
+            __syncthreads();
+        }
     }
-    const int n = (int)min((int64_t)kRankTile, M - t0);
-    for (int x = 0; x < n; ++x) {
-        const key2 v = tile[x];
-#pragma unroll
-        for (int k = 0; k < kRankPer; ++k) c[k] += (v.h > h[k]) || (v.h == h[k] && v.l > l[k]);
+    for (int x = threadIdx.x; x < kSortChunk; x += kSortThreads) {
+        skeys[c0 + x] = k[x];
+        sidx[c0 + x] = ix[x];
     }
-#pragma unroll
-    for (int k = 0; k < kRankPer; ++k)
-        if (act[k] && c[k]) atomicAdd(&rank[e0 + (int64_t)k * kTB], c[k]);
 }
 
-__global__ __launch_bounds__(kTB) void k_pack_scatter(const sw_pack_ent* all, int64_t M,
-                                                      const int32_t* rank, int32_t* order) {
-    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
-    if (e < M && all[e].st != 0) order[rank[e]] = (int32_t)e;
+__global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, const int32_t* sidx,
+                                                         int nchunks, int32_t* order) {
+    const int64_t s = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (s >= (int64_t)nchunks * kSortChunk) return;
+    const key2 v = skeys[s];
+    if (v.h == 0 && v.l == 0) return; /* inactive or padding */
+    const int c = (int)(s / kSortChunk);
+    int64_t r = s - (int64_t)c * kSortChunk;
+    for (int c2 = 0; c2 < nchunks; ++c2) {
+        if (c2 == c) continue;
+        const key2* ck = skeys + (int64_t)c2 * kSortChunk;
+        int lo = 0, hi = kSortChunk; /* first position whose key is not above v */
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (key_gt(ck[mid], v)) lo = mid + 1; else hi = mid;
+        }
+        r += lo;
+    }
+    order[r] = sidx[s];
 }
 
 /* the round loop over the global order; writes this rank's rows */
@@ -664,7 +689,7 @@ struct sw_shard_state {
     double delta = 0.0;
     ShardDev dv;
     /* device */
-    DevBuf<int32_t> w, F, E, l, taken, tie, arr[SW_A_COUNT], planned, prank, porder;
+    DevBuf<int32_t> w, F, E, l, taken, tie, arr[SW_A_COUNT], planned, porder;
     DevBuf<double> xa;
     DevBuf<double> d, R, p, xsend, xrecv;
     DevBuf<sw_jobc> jc;
@@ -675,6 +700,8 @@ struct sw_shard_state {
     DevBuf<sw_pack_ent> psend, pall;
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
+    DevBuf<key2> skeys;   /* chunk-sorted placement keys */
+    DevBuf<int32_t> sidx; /* their entries */
     /* this solve's per-job inputs on the device: the buffers above after an
      * upload, or the caller's own HBM (sw_dist_plan_solve_dev) */
     const int32_t *in_w = nullptr, *in_F = nullptr, *in_E = nullptr;
@@ -1012,11 +1039,11 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
            (int)wc, S->psend.p);
     SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr));
-    SH_HIP(S, hipMemsetAsync(S->prank.p, 0, (size_t)M * 4, st));
-    dim3 g2((unsigned)((M + kTB * kRankPer - 1) / (kTB * kRankPer)),
-            (unsigned)((M + kRankTile - 1) / kRankTile));
-    LAUNCH(S, k_pack_rank, g2, dim3(kTB), 0, st, S->pall.p, M, S->prank.p);
-    LAUNCH(S, k_pack_scatter, dim3(nblk(M)), dim3(kTB), 0, st, S->pall.p, M, S->prank.p, S->porder.p);
+    const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
+    LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, S->pall.p, M, S->skeys.p,
+           S->sidx.p);
+    LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
+           S->sidx.p, nch, S->porder.p);
     const ShardDev dv = S->dv;
     uint64_t* yd = S->y[ydst].p;
     int32_t* pd = S->arr[pdst].p;
@@ -1076,6 +1103,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     S->delta = pr->round_duration;
     const size_t NL = (size_t)std::max<int32_t>(S->NL, 1), T = (size_t)S->T;
     const size_t M = (size_t)S->P * S->world;
+    const size_t Mpad = (M + kSortChunk - 1) / kSortChunk * kSortChunk;
     const size_t xbytes = std::max<size_t>({(size_t)(2 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
     bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
                S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
@@ -1083,9 +1111,10 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
-               S->psend.reserve((size_t)S->P) || S->pall.reserve(M) || S->prank.reserve(M) ||
+               S->psend.reserve((size_t)S->P) || S->pall.reserve(M) ||
                S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64) ||
-               S->srch.reserve(4);
+               S->srch.reserve(4) ||
+               S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
     if (bad || S->hx.reserve(std::max<size_t>(xbytes * S->world, kRed * 8)))
@@ -1155,10 +1184,10 @@ void sw_shard_release(sw_handle* h) {
     if (S->comm) (void)ncclCommDestroy(S->comm);
     S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
     S->tie.release(); S->xa.release();
-    S->planned.release(); S->prank.release(); S->porder.release(); S->d.release(); S->R.release();
+    S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
-    S->caps.release(); S->hcaps.release(); S->srch.release();
+    S->caps.release(); S->hcaps.release(); S->srch.release(); S->skeys.release(); S->sidx.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
