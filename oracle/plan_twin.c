@@ -36,6 +36,7 @@ typedef struct {
     double k, A;
     const double* beta;
     const double* ell;
+    double slope[SW_BMAX];
     sw_jobc* jc;
     int32_t* Tj; /* rounds job j may use: T, or 0 if w_j > G (shockwave.py:64-75) */
     float* key;  /* [N][T] */
@@ -70,7 +71,7 @@ static double sw_detsum(const double* v, int32_t N) {
 }
 
 static double fval(const twin_t* P, int32_t j, int32_t n) {
-    return sw_f(&P->jc[j], n, P->nb, P->beta, P->ell);
+    return sw_f(&P->jc[j], n, P->nb, P->beta, P->ell, P->slope);
 }
 
 static int32_t lforce(const twin_t* P, int32_t j, double M) {
@@ -338,6 +339,7 @@ static void build(twin_t* P, const sw_problem* pr) {
     P->C = (int64_t)pr->num_gpus * T;
     P->k = pr->regularizer;
     P->beta = pr->bases; P->ell = pr->log_bases;
+    sw_pwl_slopes(P->nb, P->beta, P->ell, P->slope);
     P->passes = 0;
     size_t NN = N > 0 ? (size_t)N : 1;
     P->jc = (sw_jobc*)malloc(sizeof(sw_jobc) * NN);
@@ -353,12 +355,13 @@ static void build(twin_t* P, const sw_problem* pr) {
     }
     P->A = A;
     for (int32_t j = 0; j < N; ++j) {
+        const double ks = sw_key_scale(P->jc[j].w, A);
         double prev = fval(P, j, 0), vm = 0.0;
         for (int32_t n = 0; n < T; ++n) {
             double cur = fval(P, j, n + 1);
             double v = sw_pos(cur - prev);
             vm = (n == 0) ? v : sw_min(vm, v);
-            K_(P, j, n) = sw_key(vm, P->jc[j].w, A);
+            K_(P, j, n) = sw_key(vm, ks);
             prev = cur;
         }
     }

@@ -37,6 +37,7 @@ typedef struct {
     double k, A;
     const double* beta;
     const double* ell;
+    double slope[SW_BMAX];
     const double* p;
     sw_jobc* jc;
     int32_t* Tj;
@@ -51,7 +52,7 @@ typedef struct {
 #define KEY(E, i, n) ((E)->key[(size_t)(i) * (E)->T + (n)])
 
 static double fv(const eng_t* E, int32_t i, int32_t n) {
-    return sw_f(&E->jc[i], n, E->nb, E->beta, E->ell);
+    return sw_f(&E->jc[i], n, E->nb, E->beta, E->ell, E->slope);
 }
 
 static int32_t lforce(const eng_t* E, int32_t i, double M) {
@@ -89,12 +90,13 @@ static int e_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
     if (E->comm->allreduce_max_f64(E->comm->ctx, mx, 1)) return -1;
     E->A = mx[0];
     for (int32_t i = 0; i < E->NL; ++i) {
+        const double ks = sw_key_scale(E->jc[i].w, E->A);
         double prev = fv(E, i, 0), vm = 0.0;
         for (int32_t n = 0; n < E->T; ++n) {
             double cur = fv(E, i, n + 1);
             double v = sw_pos(cur - prev);
             vm = (n == 0) ? v : sw_min(vm, v);
-            KEY(E, i, n) = sw_key(vm, E->jc[i].w, E->A);
+            KEY(E, i, n) = sw_key(vm, ks);
             prev = cur;
         }
         mx[1] = sw_max(mx[1], sw_g(&E->jc[i], E->Tj[i]));
@@ -413,6 +415,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     E.k = local->regularizer;
     E.beta = local->bases;
     E.ell = local->log_bases;
+    sw_pwl_slopes(E.nb, E.beta, E.ell, E.slope);
     E.p = local->priority;
     E.res = res;
     const size_t NN = E.NL > 0 ? (size_t)E.NL : 1;

@@ -62,6 +62,7 @@ typedef struct {
     double a;    /* p / (N·T)              */
     double Fd;   /* F as double            */
     double Ed;   /* E as double            */
+    double invE; /* 1 / E                  */
     int32_t w;   /* nworkers               */
 } sw_jobc;
 
@@ -75,6 +76,7 @@ SW_HD sw_jobc sw_make_jobc(int32_t N, int32_t T, double delta, int32_t w, double
     c.a = p / ((double)N * (double)T);
     c.Fd = (double)F;
     c.Ed = (double)E;
+    c.invE = 1.0 / (double)E;
     c.w = w;
     return c;
 }
@@ -91,33 +93,44 @@ SW_HD double sw_g(const sw_jobc* c, int32_t n) {
     return v > 0.0 ? v : 0.0;
 }
 
+/* Segment slopes of the log interpolation, once per problem:
+ * slope_b = (ℓ_{b+1} − ℓ_b) / (β_{b+1} − β_b), 0 past the last segment. */
+SW_HD void sw_pwl_slopes(int32_t nb, const double* beta, const double* ell, double* slope) {
+    for (int32_t b = 0; b < SW_BMAX; ++b)
+        slope[b] = b < nb - 1 ? (ell[b + 1] - ell[b]) / (beta[b + 1] - beta[b]) : 0.0;
+}
+
 /* φ(u): interpolation of log over the bases on the segment holding u
- * (segment = largest b ≤ nb-2 with β_b ≤ u). */
-SW_HD double sw_phi(double u, int32_t nb, const double* beta, const double* ell) {
+ * (segment = largest b ≤ nb-2 with β_b ≤ u): ℓ_b + slope_b·(u − β_b), the
+ * reference's ω-weighted sum of the two breakpoints (shockwave.py:162-181)
+ * up to rounding, with no division per evaluation. */
+SW_HD double sw_phi(double u, int32_t nb, const double* beta, const double* ell,
+                    const double* slope) {
     int32_t b = 0;
     for (int32_t i = 1; i < nb - 1; ++i)
         if (beta[i] <= u) b = i;
-    double t = (u - beta[b]) / (beta[b + 1] - beta[b]);
-    return ell[b] + (ell[b + 1] - ell[b]) * t;
+    return ell[b] + slope[b] * (u - beta[b]);
 }
 
 /* f(n) — weighted log-utility with n planned rounds. */
 SW_HD double sw_f(const sw_jobc* c, int32_t n, int32_t nb, const double* beta,
-                  const double* ell) {
-    double u = (c->Fd + sw_e(c, n)) / c->Ed;
-    return c->a * sw_phi(u, nb, beta, ell);
+                  const double* ell, const double* slope) {
+    double u = (c->Fd + sw_e(c, n)) * c->invE;
+    return c->a * sw_phi(u, nb, beta, ell, slope);
 }
 
 /*
  * Ranking key of the job's (n+1)-th planned round: the monotonised marginal
  * utility per GPU-round, normalised by A = max_j a_j and rounded to fp32:
  *   vm(n) = min(vm(n−1), max(0, f(n+1) − f(n)))       (nonincreasing in n)
- *   key(n) = fp32(vm(n) / (w·A)), flushed to 0 below FLT_MIN.
+ *   key(n) = fp32(vm(n) · s), s = 1 / (w·A) once per job (sw_key_scale),
+ *   flushed to 0 below FLT_MIN.
  * Keys are ≥ +0, so their bit patterns order like their values.
  */
-SW_HD float sw_key(double vm, int32_t w, double A) {
-    if (!(A > 0.0)) return 0.0f;
-    double k = vm / ((double)w * A);
+SW_HD double sw_key_scale(int32_t w, double A) { return A > 0.0 ? 1.0 / ((double)w * A) : 0.0; }
+
+SW_HD float sw_key(double vm, double scale) {
+    double k = vm * scale;
     if (k < SW_FLT_MIN) return 0.0f;
     if (k > SW_FLT_MAX) k = SW_FLT_MAX;
     return (float)k;

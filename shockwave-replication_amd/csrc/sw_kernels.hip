@@ -75,6 +75,7 @@ struct Ctx {
     const sw_inst_dev* inst;
     const double* beta; /* LDS */
     const double* ell;  /* LDS */
+    const double* slope; /* LDS: segment slopes (sw_pwl_slopes) */
     sw_blk blk;
     /* inputs (instance-relative) */
     const int32_t* w_in;
@@ -133,7 +134,7 @@ struct Ctx {
     }
     __device__ __forceinline__ int Tj(int j, int s) const { return jc(j, s).w <= G ? T : 0; }
     __device__ __forceinline__ double fval(int j, int s, int n) const {
-        return sw_f(&jc(j, s), n, nb, beta, ell);
+        return sw_f(&jc(j, s), n, nb, beta, ell, slope);
     }
     __device__ __forceinline__ double gval(int j, int s, int n) const {
         return sw_g(&jc(j, s), n);
@@ -213,12 +214,13 @@ struct Ctx {
              * per thread per chunk), then compile-time-indexed copies */
             constexpr int CH = 4;
             float* stage = reinterpret_cast<float*>(sbuf);
-            double prev[SW_JPT], vm[SW_JPT];
+            double prev[SW_JPT], vm[SW_JPT], ksc[SW_JPT];
 #pragma unroll
             for (int s = 0; s < SW_JPT; ++s) {
                 prev[s] = 0.0;
                 vm[s] = 0.0;
-                if (s < q && jlo() + s < N) prev[s] = sw_f(&jcs[s], 0, nb, beta, ell);
+                ksc[s] = sw_key_scale(jcs[s].w, A);
+                if (s < q && jlo() + s < N) prev[s] = sw_f(&jcs[s], 0, nb, beta, ell, slope);
             }
 #pragma unroll
             for (int ch = 0; ch < KT / CH; ++ch) {
@@ -229,10 +231,10 @@ struct Ctx {
                         const int n = ch * CH + i;
                         float kv = 0.0f;
                         if (act && n < T && jcs[s].w <= G) {
-                            const double cur = sw_f(&jcs[s], n + 1, nb, beta, ell);
+                            const double cur = sw_f(&jcs[s], n + 1, nb, beta, ell, slope);
                             const double v = sw_pos(cur - prev[s]);
                             vm[s] = (n == 0) ? v : sw_min(vm[s], v);
-                            kv = sw_key(vm[s], jcs[s].w, A);
+                            kv = sw_key(vm[s], ksc[s]);
                             prev[s] = cur;
                         }
                         stage[(s * CH + i) * SW_BLOCK + threadIdx.x] = kv;
@@ -247,13 +249,13 @@ struct Ctx {
         } else {
             for (int j = jlo(); j < jhi(); ++j) {
                 const sw_jobc& c = gjc[j];
-                double prev = sw_f(&c, 0, nb, beta, ell), vm = 0.0;
+                double prev = sw_f(&c, 0, nb, beta, ell, slope), vm = 0.0;
                 float* row = gkeys + (size_t)j * KT;
                 for (int n = 0; n < T; ++n) {
-                    const double cur = sw_f(&c, n + 1, nb, beta, ell);
+                    const double cur = sw_f(&c, n + 1, nb, beta, ell, slope);
                     const double v = sw_pos(cur - prev);
                     vm = (n == 0) ? v : sw_min(vm, v);
-                    row[n] = sw_key(vm, c.w, A);
+                    row[n] = sw_key(vm, sw_key_scale(c.w, A));
                     prev = cur;
                 }
             }
@@ -922,9 +924,10 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     };
     c.blk.X = (sw_xchg*)carve(sizeof(sw_xchg));
     c.blk.par = 0;
-    double* bt = (double*)carve(sizeof(double) * 2 * SW_BMAX);
+    double* bt = (double*)carve(sizeof(double) * 3 * SW_BMAX);
     c.beta = bt;
     c.ell = bt + SW_BMAX;
+    c.slope = bt + 2 * SW_BMAX;
     c.PL = (sw_pack_lds*)carve(sizeof(sw_pack_lds));
     c.H = c.PL->H[0];
     c.SH = c.PL->SH[0];
@@ -932,8 +935,12 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.pwc = 0;
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
     if (threadIdx.x < SW_BMAX) {
-        bt[threadIdx.x] = I->beta[threadIdx.x];
-        bt[SW_BMAX + threadIdx.x] = I->ell[threadIdx.x];
+        const int b = (int)threadIdx.x;
+        bt[b] = I->beta[b];
+        bt[SW_BMAX + b] = I->ell[b];
+        /* sw_pwl_slopes, one segment per thread (same IEEE division) */
+        bt[2 * SW_BMAX + b] = b < I->nb - 1 ? (I->ell[b + 1] - I->ell[b]) / (I->beta[b + 1] - I->beta[b])
+                                            : 0.0;
     }
     if constexpr (ONE) {
         const int NJ = SW_LDS_JOBS;

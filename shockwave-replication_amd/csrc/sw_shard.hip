@@ -78,7 +78,7 @@ struct ShardDev {
     int32_t NL, T, G, nb, LW, rank;
     int64_t off, N, q, P;
     double k;
-    double beta[SW_BMAX], ell[SW_BMAX];
+    double beta[SW_BMAX], ell[SW_BMAX], slope[SW_BMAX];
     const sw_jobc* jc;
     float* keys;
     const double* p;
@@ -169,13 +169,14 @@ __global__ __launch_bounds__(kTB) void k_keys(ShardDev S) {
     if (i >= S.NL) return;
     const double A = sw_from_bits((uint64_t)S.red[0]);
     const sw_jobc c = S.jc[i];
+    const double ks = sw_key_scale(c.w, A);
     float* row = S.keys + (size_t)i * S.T;
-    double prev = sw_f(&c, 0, S.nb, S.beta, S.ell), vm = 0.0;
+    double prev = sw_f(&c, 0, S.nb, S.beta, S.ell, S.slope), vm = 0.0;
     for (int n = 0; n < S.T; ++n) {
-        const double cur = sw_f(&c, n + 1, S.nb, S.beta, S.ell);
+        const double cur = sw_f(&c, n + 1, S.nb, S.beta, S.ell, S.slope);
         const double v = sw_pos(cur - prev);
         vm = (n == 0) ? v : sw_min(vm, v);
-        row[n] = sw_key(vm, c.w, A);
+        row[n] = sw_key(vm, ks);
         prev = cur;
     }
 }
@@ -427,14 +428,14 @@ __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const in
         const sw_jobc c = S.jc[i];
         if (sel == SW_EV_SELECT) {
             const int n = S.arr[SW_A_N][i];
-            fa = sw_f(&c, n, S.nb, S.beta, S.ell);
-            fb = sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell);
+            fa = sw_f(&c, n, S.nb, S.beta, S.ell, S.slope);
+            fb = sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell, S.slope);
             gm = sw_g(&c, n);
         } else if (sel == SW_EV_GMAX) {
             gm = sw_g(&c, arr[i]);
         } else if (sel == SW_EV_PACKED) {
             const int pl = arr[i];
-            fa = sw_f(&c, pl, S.nb, S.beta, S.ell);
+            fa = sw_f(&c, pl, S.nb, S.beta, S.ell, S.slope);
             gm = sw_g(&c, pl);
             is = (long long)c.w * (S.arr[SW_A_NB][i] - pl);
         } else if (sel == SW_EV_P2OK) {
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const in
                 row[t] = (uint8_t)bit;
             }
             S.planned[i] = cn;
-            fa = sw_f(&c, cn, S.nb, S.beta, S.ell);
+            fa = sw_f(&c, cn, S.nb, S.beta, S.ell, S.slope);
             fb = cn > 0 ? ((double)Ssum / (double)cn) * S.p[i] : 0.0;
             gm = sw_g(&c, cn);
             is = cn > 0;
@@ -1147,6 +1148,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
         v.beta[b] = b < pr->num_bases ? pr->bases[b] : 0.0;
         v.ell[b] = b < pr->num_bases ? pr->log_bases[b] : 0.0;
     }
+    sw_pwl_slopes(pr->num_bases, pr->bases, pr->log_bases, v.slope);
     v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->in_p; v.l = S->l.p; v.taken = S->taken.p;
     v.tie = S->tie.p; v.xa = S->xa.p;
     for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
