@@ -42,7 +42,7 @@ namespace {
         __syncthreads();                                                          \
         if (threadIdx.x == 0 && B.stamps) {                                       \
             uint64_t now_ = __builtin_amdgcn_s_memtime();                         \
-            B.stamps[(size_t)blockIdx.x * 16 + (slot)] += now_ - stamp_prev_;      \
+            B.stamps[(size_t)inst_ * 16 + (slot)] += now_ - stamp_prev_;      \
             stamp_prev_ = now_;                                                   \
         }                                                                         \
     } while (0)
@@ -895,9 +895,28 @@ struct Ctx {
     }
 };
 
+/* Dynamic LDS of the plan kernel: the carve-up in solve_instance, region by
+ * region (16-byte aligned).  The launch sizes the allocation with it and the
+ * kernel compares its own carve offset against it (constant-folded). */
+__host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
+    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t s = r16(sizeof(sw_xchg)) + r16(sizeof(double) * 3 * SW_BMAX) +
+               r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8);
+    if (one) {
+        const size_t NJ = SW_LDS_JOBS;
+        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
+    }
+    return s;
+}
+
 template <int KT, bool ONE>
-__device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned char* smem) {
-    const sw_inst_dev* I = &B.inst[blockIdx.x];
+__device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned char* smem,
+                                                         int inst_) {
+    const sw_inst_dev* I = &B.inst[inst_];
+#ifdef SW_STAMPS
+    /* placement diagnostics: 100 MHz wall clock at entry / exit, HW_ID, XCC_ID */
+    const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
+#endif
     Ctx<KT, ONE> c;
     c.inst = I;
     c.N = I->N;
@@ -912,7 +931,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     const int64_t jo = I->job_off;
     c.w_in = B.w + jo;
 #ifdef SW_STAMPS
-    c.swp = B.stamps ? B.stamps + (size_t)blockIdx.x * 16 + 8 : nullptr;
+    c.swp = B.stamps ? B.stamps + (size_t)inst_ * 16 + 8 : nullptr;
 #endif
     c.p_in = B.p + jo;
 
@@ -992,6 +1011,8 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             c.gjc[j] = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
                                     B.E[jo + j], B.R[jo + j], B.p[jo + j]);
     }
+    /* folds away when the carve-up matches the launch's allocation */
+    if (off != sw_plan_lds_bytes(ONE)) __builtin_trap();
     __syncthreads();
 
 #ifdef SW_STAMPS
@@ -1159,29 +1180,34 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         o.bound = bound;
         o.iters = (int32_t)c.passes;
         o.status = status;
-        B.out[blockIdx.x] = o;
+        B.out[inst_] = o;
+#ifdef SW_STAMPS
+        if (B.stamps) {
+            uint64_t* st = B.stamps + (size_t)inst_ * 16;
+            st[6] = ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                    (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+            st[7] = rt0_;
+            st[14] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
     }
 }
 
 }  // namespace
 
+/* One workgroup per instance.  A persistent work-queue variant (each
+ * workgroup pulling instances from a device counter) removed the dispatch
+ * gaps between workgroups on a CU but not the tail, which is set by the
+ * expensive instances taken last, and its loop cost registers: the same
+ * throughput and a slower single solve. */
 template <int KT, bool ONE>
 __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
-    solve_instance<KT, ONE>(B, sw_smem);
+    solve_instance<KT, ONE>(B, sw_smem, blockIdx.x);
 }
 
-/* LDS bytes the kernel needs (must match the carve-up above). */
-extern "C" size_t sw_plan_kernel_lds_bytes(int one) {
-    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t s = r16(sizeof(sw_xchg)) + r16(sizeof(double) * 2 * SW_BMAX) +
-               r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8);
-    if (one) {
-        const size_t NJ = SW_LDS_JOBS;
-        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
-    }
-    return s;
-}
+/* LDS bytes the kernel needs (solve_instance checks its carve-up against it). */
+extern "C" size_t sw_plan_kernel_lds_bytes(int one) { return sw_plan_lds_bytes(one != 0); }
 
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream) {

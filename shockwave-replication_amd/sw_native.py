@@ -328,7 +328,8 @@ def load(path: str | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    # SW_LIB_PATH: an alternative in-tree build (A/B experiments, tools/)
+    p = path or os.environ.get("SW_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise NativeError(
             f"{p} not found: build it with `python __graft_entry__.py build` "
