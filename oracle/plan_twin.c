@@ -127,13 +127,31 @@ static int select_level(twin_t* P, double M, int is_inf, int32_t* n, int32_t* l,
         for (int32_t j = 0; j < N; ++j) { n[j] = P->Tj[j]; taken[j] = P->Tj[j] - l[j]; }
         wgt_star = Wall;
     } else {
+        /* Bisection snapped to key values.  A job's count is a function of
+         * its raw count #{n < Tj : key > ρ}, which only changes at its key
+         * values; so with mx = the largest key ≤ mid and mn = the smallest
+         * key > mid over the jobs whose count still varies on [lo, hi]
+         * ("open": cnt_ge(lo) ≠ cnt_gt(hi)), W is constant on [mx, mid] and
+         * on [mid, mn).  A probe below budget moves hi to max(lo, mx), one
+         * above it moves lo to min(hi, mn): same ρ* as the plain bisection,
+         * fewer probes. */
         uint32_t lo = plo, hi = phi;
         while (lo < hi) {
             uint32_t mid = lo + ((hi - lo) >> 1);
             int64_t wg = 0;
-            for (int32_t j = 0; j < N; ++j) wg += (int64_t)P->jc[j].w * cnt_gt(P, j, mid, l[j]);
+            uint32_t mx = 0, mn = 0x7FFFFFFFu;
+            for (int32_t j = 0; j < N; ++j) {
+                wg += (int64_t)P->jc[j].w * cnt_gt(P, j, mid, l[j]);
+                if (cnt_ge(P, j, lo, l[j]) == cnt_gt(P, j, hi, l[j])) continue;
+                for (int32_t q = 0; q < P->Tj[j]; ++q) {
+                    const uint32_t b = sw_fbits_of(K_(P, j, q));
+                    if (b > mid) mn = b < mn ? b : mn;
+                    else mx = b > mx ? b : mx;
+                }
+            }
             P->passes++;
-            if (wg <= bud) hi = mid; else lo = mid + 1;
+            if (wg <= bud) hi = mx > lo ? mx : lo;
+            else lo = mn < hi ? mn : hi;
         }
         uint32_t rho = lo;
         ev->rho = rho;

@@ -260,6 +260,34 @@ struct sw_blk {
         MN = b;
     }
 
+    /* Σ v, max mx and min mn of non-negative 32-bit values, one barrier
+     * (the snapped price bisection: weighted count and the two key bits
+     * that bound the step of W around the probe). */
+    __device__ __forceinline__ int32_t sum32_max_min(int32_t v, int32_t mx, int32_t mn, int32_t& MX,
+                                                     int32_t& MN) {
+        v = wave_sum_i32(v);
+        mx = wave_max_i32(mx);
+        mn = wave_min_i32(mn);
+        if (lane_id() == 0) {
+            X->i[par][wave_id()][0] = v;
+            X->i[par][wave_id()][1] = (int64_t)(((uint64_t)(uint32_t)mx << 32) | (uint32_t)mn);
+        }
+        __syncthreads();
+        int32_t t = 0, a = 0, b = 0x7FFFFFFF;
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) {
+            t += (int32_t)X->i[par][w][0];
+            const uint64_t p = (uint64_t)X->i[par][w][1];
+            const int32_t pm = (int32_t)(p >> 32), pn = (int32_t)(uint32_t)p;
+            a = pm > a ? pm : a;
+            b = pn < b ? pn : b;
+        }
+        flip();
+        MX = a;
+        MN = b;
+        return t;
+    }
+
     /* sw_detsum of the per-thread partials v, and the max of m, together. */
     __device__ __forceinline__ void detsum_max(double v, double m, double& S, double& M) {
         v = wave_dettree(v);

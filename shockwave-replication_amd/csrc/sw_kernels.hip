@@ -204,6 +204,47 @@ struct Ctx {
         return c;
     }
 
+    /* cnt<false>(ρ = mid) of an open job, plus its key bits around mid:
+     * mx = max(mx, largest key ≤ mid), mn = min(mn, smallest key > mid)
+     * (twin: the snapped bisection of select_level).  The row is
+     * nonincreasing, so the raw count c0 splits it there. */
+    __device__ __forceinline__ int cnt_snap(int j, int s, uint32_t mid, int l, int32_t& mx,
+                                            int32_t& mn) const {
+        const int tj = Tj(j, s);
+        int c = 0;
+        if constexpr (ONE) {
+            (void)j;
+            /* the keys > mid are the prefix [0, c0): the last of them is
+             * row[c0 − 1] and the key after it row[c0] (0 past the row), so
+             * two selects on the compare, no min / max per key */
+            uint32_t lo_k = 0x7FFFFFFFu, hi_k = sw_fbits_of(kr[s][0]);
+#pragma unroll
+            for (int n = 0; n < KT; ++n) {
+                const uint32_t b = sw_fbits_of(kr[s][n]);
+                const uint32_t nx = n + 1 < KT ? sw_fbits_of(kr[s][n + 1 < KT ? n + 1 : n]) : 0u;
+                const bool gt = b > mid;
+                c += gt ? 1 : 0;
+                lo_k = gt ? b : lo_k;
+                hi_k = gt ? nx : hi_k;
+            }
+            mn = min(mn, (int32_t)lo_k);
+            mx = max(mx, (int32_t)hi_k);
+        } else {
+            (void)s;
+            const float* row = gkeys + (size_t)j * KT;
+            int lo = 0, hi = tj;
+            while (lo < hi) {
+                const int m = (lo + hi) >> 1;
+                if (sw_fbits_of(row[m]) > mid) lo = m + 1; else hi = m;
+            }
+            c = lo;
+            if (c < tj) mx = max(mx, (int32_t)sw_fbits_of(row[c]));
+            if (c > 0) mn = min(mn, (int32_t)sw_fbits_of(row[c - 1]));
+        }
+        c = (c < tj ? c : tj) - l;
+        return c > 0 ? c : 0;
+    }
+
     /* twin: build() — constants and key rows */
     __device__ __forceinline__ void setup() {
         double amax = 0.0;
@@ -309,16 +350,22 @@ struct Ctx {
                         ca[s] = cnt<true>(j, s, lo, lcur[j]);
                         cb[s] = cnt<false>(j, s, hi, lcur[j]);
                     });
+                /* Snapped to key values (twin: select_level): the open
+                 * jobs also report the keys either side of mid, W is
+                 * constant between them, and the bracket jumps there.
+                 * ca / cb stay exact: no open job has a key strictly
+                 * between the snapped end and mid. */
                 while (lo < hi) {
                     const uint32_t mid = lo + ((hi - lo) >> 1);
-                    int32_t wg = 0;
+                    int32_t wg = 0, mx = 0, mn = 0x7FFFFFFF;
                     for_jobs([&](int j, int s) {
                         int c = cb[s];
-                        if (ca[s] != cb[s]) c = cnt<false>(j, s, mid, lcur[j]);
+                        if (ca[s] != cb[s]) c = cnt_snap(j, s, mid, lcur[j], mx, mn);
                         cm[s] = c;
                         wg += jc(j, s).w * c;
                     });
-                    wg = blk.sum32(wg);
+                    int32_t MX, MN;
+                    wg = blk.sum32_max_min(wg, mx, mn, MX, MN);
                     passes++;
                     const bool down = wg <= bud;
 #pragma unroll
@@ -326,16 +373,25 @@ struct Ctx {
                         cb[s] = down ? cm[s] : cb[s];
                         ca[s] = down ? ca[s] : cm[s];
                     }
-                    if (down) hi = mid; else lo = mid + 1;
+                    if (down) hi = (uint32_t)MX > lo ? (uint32_t)MX : lo;
+                    else lo = (uint32_t)MN < hi ? (uint32_t)MN : hi;
                 }
             } else {
                 while (lo < hi) {
                     const uint32_t mid = lo + ((hi - lo) >> 1);
-                    int32_t wg = 0;
-                    for_jobs([&](int j, int s) { wg += jc(j, s).w * cnt<false>(j, s, mid, lcur[j]); });
-                    wg = blk.sum32(wg);
+                    int32_t wg = 0, mx = 0, mn = 0x7FFFFFFF;
+                    for_jobs([&](int j, int s) {
+                        const int l = lcur[j];
+                        if (cnt<true>(j, s, lo, l) != cnt<false>(j, s, hi, l))
+                            wg += jc(j, s).w * cnt_snap(j, s, mid, l, mx, mn);
+                        else
+                            wg += jc(j, s).w * cnt<false>(j, s, mid, l);
+                    });
+                    int32_t MX, MN;
+                    wg = blk.sum32_max_min(wg, mx, mn, MX, MN);
                     passes++;
-                    if (wg <= bud) hi = mid; else lo = mid + 1;
+                    if (wg <= bud) hi = (uint32_t)MX > lo ? (uint32_t)MX : lo;
+                    else lo = (uint32_t)MN < hi ? (uint32_t)MN : hi;
                 }
             }
             const uint32_t rho = lo;
