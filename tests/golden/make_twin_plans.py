@@ -1,0 +1,53 @@
+"""Generates tests/golden/twin_plans.json: plan digests of the CPU twin
+(oracle/plan_twin.c) on seeded instances at the three reference cluster
+configurations (scale_{64,128,256}gpus.json's k and lambda), with the price
+bisection over plain fp32 key bits (the twin as of commit aed1d81).
+
+The snapped price search must return the same rho* and so
+the same plans; tests/test_twin_plans.py checks the current twin against
+these digests.  Regenerate (only when the algorithm is meant to change):
+
+    git show aed1d81:oracle/plan_twin.c > /tmp/old_twin/plan_twin.c
+    (plus sw_arith.h etc. from the same commit, see build_old below)
+    python tests/golden/make_twin_plans.py /tmp/old_twin/libplan_twin.so
+"""
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "shockwave-replication_amd")]
+import sw_native as sn  # noqa: E402
+import sw_synth as ss  # noqa: E402
+
+# (G, k, lambda, N, T): scale_256gpus.json, scale_128gpus.json, scale_64gpus.json
+CONFIGS = [(256, 1e5, 5.0, 900, 30), (128, 1e-3, 15.0, 300, 30), (64, 10.0, 5.0, 300, 20),
+           (32, 1e5, 5.0, 50, 20)]
+SEEDS = range(8)
+
+
+def digest(lib_path):
+    lib = ctypes.CDLL(lib_path)
+    sn.declare_solver_api(lib, "twin_")
+    out = []
+    for G, k, lam, N, T in CONFIGS:
+        for seed in SEEDS:
+            a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+            b = sn.ProblemArrays(a.w, a.d, a.F, a.E, a.R, a.p, a.T, a.G, a.delta, a.k, tuple(a.bases))
+            pr, res = b.c_problem(), b.c_result()
+            rc = lib.twin_plan_solve(ctypes.byref(pr), ctypes.byref(res))
+            out.append({"G": G, "k": k, "lam": lam, "N": N, "T": T, "seed": seed, "rc": int(rc),
+                        "objective": float(res.objective).hex(),
+                        "plan_md5": hashlib.md5(b.plan.tobytes()).hexdigest(),
+                        "counts_md5": hashlib.md5(b.planned.tobytes()).hexdigest()})
+    return out
+
+
+if __name__ == "__main__":
+    rows = digest(sys.argv[1])
+    json.dump({"source": "oracle/plan_twin.c at aed1d81 (plain price bisection)", "cases": rows},
+              open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "twin_plans.json"), "w"),
+              indent=0)
+    print(len(rows), "cases")
