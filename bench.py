@@ -77,9 +77,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=2048,
-                    help="instances per GPU per step (8 per CU: one 512-thread workgroup fits a "
-                         "CU at a time, so per-instance work differences average out, DESIGN.md §6)")
+    ap.add_argument("--batch", type=int, default=8192,
+                    help="instances per GPU per step (32 per CU: one 512-thread workgroup fits a "
+                         "CU at a time; a launch ends with its most expensive instances running "
+                         "alone, ~0.75 ms, so more instances per launch amortise that tail, "
+                         "DESIGN.md §6)")
     ap.add_argument("--jobs", type=int, default=900)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--seed", type=int, default=0)
