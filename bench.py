@@ -31,7 +31,8 @@ sys.path.insert(0, PKG)
 import sw_native as sn  # noqa: E402
 import sw_synth as ss  # noqa: E402
 
-HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+HBM_PEAK = 8.0e12
+C4_SEED = 77  # the C4 instance of the sub-record (tests/golden/c4_digest.json)  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 
 # The result line is the only thing on stdout: libraries (RCCL prints its
 # version banner on communicator init) write to fd 1 directly, so fd 1 is
@@ -43,13 +44,29 @@ def emit(line: dict):
     print(json.dumps(line), file=_RESULT_OUT or sys.stdout, flush=True)
 
 
+# Dominant kernel sw_plan_kernel: bytes that MUST cross HBM per instance
+# (DESIGN.md §6): the SoA inputs (w i32, d f64, F i32, E i32, R f64, p f64 =
+# 36 B per job, sw_synth / include/shockwave_amd.h) and the instance descriptor
+# (sw_inst_dev, 176 B) in; the 0/1 plan (N·T B), the planned-round counts
+# (4 B per job) and the result record (sw_out_dev, 48 B) out.
+INST_DESC_BYTES = 176
+RESULT_BYTES = 48
+CLOCK_HZ = 2.4e9  # MI355X engine clock (MI355X_MICROARCH.md)
+NUM_CU = 256
+
+
+def algorithmic_bytes(N: int, T: int) -> int:
+    """HBM bytes one plan solve must move (inputs in, plan + counts + result out)."""
+    return 36 * N + INST_DESC_BYTES + N * T + 4 * N + RESULT_BYTES
+
+
 def pass_bytes(N: int, T: int) -> int:
-    """Algorithmic bytes of one pass of the plan kernel over an instance's jobs.
+    """On-chip bytes of one pass of the plan kernel over an instance's jobs.
 
     Every price/level/packing pass reads each job's fp32 key row (4·T B) and
-    its constants/state (32 B: rate, cap, R, d as the 8-B values a pass
-    touches), per DESIGN.md §4.  The analogue of SURVEY.md §8(d)'s B_iter for
-    this kernel; the working set stays on chip (VGPR/LDS).
+    its constants/state (32 B), per DESIGN.md §4.  This working set stays in
+    VGPRs/LDS and never touches HBM, so it is reported as on-chip throughput,
+    not against the HBM roofline.
     """
     return 4 * N * T + 32 * N
 
@@ -91,6 +108,10 @@ def parse():
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
                     help="c3: batched 900x30 instances per GPU (headline, replicas); "
                          "c4: one 10k x 30 instance sharded across the ranks (RCCL)")
+    ap.add_argument("--c4-steps", dest="c4_steps", type=int, default=20,
+                    help="sharded C4 solves timed for the c4_sharded sub-record")
+    ap.add_argument("--no-c4", dest="no_c4", action="store_true",
+                    help="skip the sharded C4 sub-record of the default line")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -250,37 +271,31 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # single-instance latency (a scheduler's call pattern), rank 0 only
-    lat_ms = None
-    if rank == 0:
-        one = sn.Solver(device=local)
-        one.upload(batch[:1])
-        one.run()
-        one.download()
-        t1 = time.perf_counter()
-        reps = 20
-        for _ in range(reps):
-            one.run()
-        one.download()
-        lat_ms = (time.perf_counter() - t1) / reps * 1e3
-        one.close()
-
     total = args.steps * args.batch * world
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     avg_kernel_s = (ms_plan / max(runs, 1)) / 1e3
-    alg_bytes = float(np.sum(iters) * pass_bytes(args.jobs, args.rounds))
+    alg_bytes = float(args.batch * algorithmic_bytes(args.jobs, args.rounds))
     achieved = alg_bytes / avg_kernel_s if avg_kernel_s > 0 else 0.0
-
+    onchip = float(np.sum(iters) * pass_bytes(args.jobs, args.rounds))
     traffic = pmc_traffic(args.batch, args.jobs, args.rounds)
+
+    extra = {}
     if rank == 0:
-        cpu = None
-        if args.cpu_baseline:
-            try:
-                cpu = cpu_baseline(args)
-            except Exception as e:  # reported, never silently substituted
-                cpu = {"value": None, "unit": "plan-solves/s", "cores": 1, "kind": "port",
-                       "sample": f"failed: {e!r}"}
+        extra = boundary_legs(args, solver, batch, results, local)
+    solver.close()
+    cpu = None
+    if rank == 0 and args.cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as e:  # reported, never silently substituted
+            cpu = {"value": None, "unit": "plan-solves/s", "cores": 1, "kind": "port",
+                   "sample": f"failed: {e!r}"}
+    c4 = None
+    if not args.no_c4:
+        c4 = c4_leg(args, world, rank, local, dist)
+    if rank == 0:
+        cyc = avg_kernel_s * CLOCK_HZ * min(NUM_CU, args.batch) / args.batch
         line = {
             "metric": "Shockwave plan solves/sec at 900 jobs x 30 rounds",
             "value": value,
@@ -292,7 +307,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64 objective / fp32 ranking keys",
             "data": "synthetic (seeded C3-shaped instances; reference trace pickles are missing)",
             "config": {
                 "workload": f"C3 plan solve: {args.jobs} jobs x {args.rounds} rounds, G=256, "
@@ -307,22 +322,157 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic[0] if traffic else None,
-                "traffic_source": traffic[1] if traffic else None,
-                "note": ("achieved counts the per-pass working set, which stays on chip "
-                         "(VGPR/LDS); traffic is the HBM side (PMC). DESIGN.md §6"),
+                "traffic_source": (f"{traffic[1]} (rocprofv3 PMC pass of this workload, "
+                                   "FETCH_SIZE x2 + WRITE_SIZE)") if traffic else None,
                 "kernel": "sw_plan_kernel",
                 "avg_kernel_ms": avg_kernel_s * 1e3,
-                "passes_per_instance": float(np.mean(iters)),
-                "bytes_per_pass": pass_bytes(args.jobs, args.rounds),
+                "algorithmic_bytes_per_instance": algorithmic_bytes(args.jobs, args.rounds),
+                "note": ("achieved = bytes a solve must move through HBM (inputs in; plan, counts, "
+                         "result out) / kernel time.  The kernel is NOT HBM-bound: its working "
+                         "set stays in VGPRs/LDS and it is latency-bound on block barriers "
+                         "(DESIGN.md §6); see onchip and cycles_per_instance"),
             },
+            "onchip": {
+                "bytes_per_pass": pass_bytes(args.jobs, args.rounds),
+                "passes_per_instance": float(np.mean(iters)),
+                "bytes_per_s": onchip / avg_kernel_s if avg_kernel_s > 0 else 0.0,
+                "what": "key rows + per-job state re-read from VGPR/LDS by every search / pack pass",
+            },
+            "cycles_per_instance": cyc,
+            "cycles_note": (f"avg kernel time x {CLOCK_HZ / 1e9:g} GHz x {NUM_CU} CUs / instances: "
+                            "CU-cycles one solve occupies (one 512-thread workgroup per CU)"),
             "cpu_baseline": cpu,
-            "single_instance_ms": lat_ms,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }
+        line.update(extra)
+        if c4 is not None:
+            line["c4_sharded"] = c4
         emit(line)
-    solver.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def boundary_legs(args, solver, batch, results, local):
+    """The host-buffer boundary (rank 0): what a caller of the C-ABI with host
+    arrays sees (shockwave.py:381-398 is a synchronous host call).
+
+    * host_boundary_solves_per_s — sw_plan_solve_batch on the same instances:
+      pack + upload over PCIe, the kernel, plans and results back;
+    * single_instance_ms — one sw_plan_solve per call (the scheduler's call
+      pattern: host arrays in, plan out), averaged over repeated calls;
+    * sustained_solves_per_s — device-resident launches back to back for ~2 s
+      (keeps the GPU busy long enough for outside utilisation sampling).
+    """
+    out = {}
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rb = solver.solve_batch(batch)
+    dt = time.perf_counter() - t0
+    assert all(np.array_equal(a["plan"], b["plan"]) for a, b in zip(rb[:64], results[:64]))
+    out["host_boundary_solves_per_s"] = reps * len(batch) / dt
+    out["host_boundary_ms_per_batch"] = dt / reps * 1e3
+    one = sn.Solver(device=local)
+    a = batch[0]
+    one.solve(a)
+    n1 = 50
+    t0 = time.perf_counter()
+    for _ in range(n1):
+        r1 = one.solve(a)
+    out["single_instance_ms"] = (time.perf_counter() - t0) / n1 * 1e3
+    assert np.array_equal(r1["plan"], results[0]["plan"])
+    one.close()
+    solver.upload(batch)
+    import torch
+
+    torch.cuda.synchronize()
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(20):
+            solver.run()
+        torch.cuda.synchronize()
+        n += 20
+        if time.perf_counter() - t0 > 2.0:
+            break
+    out["sustained_solves_per_s"] = n * len(batch) / (time.perf_counter() - t0)
+    return out
+
+
+def c4_leg(args, world, rank, local, dist):
+    """The C4 sub-record: ONE 10,000-job × 30-round
+    instance with its jobs sharded over the N ranks of this run
+    (sw_dist_shard_range), every step's counts / maxima all-reduced and the
+    lane sums / placement keys all-gathered through RCCL on the handle's
+    stream — RCCL runs at N = 1 too.  Inputs and the plan stay in HBM; total
+    work is fixed, so across the driver's N = 1, 2, 4, 8 runs this is strong
+    scaling.  The result is checked against the committed digest of the CPU
+    twin's solve of the same instance (tests/golden/c4_digest.json)."""
+    import hashlib
+
+    import torch
+
+    c = ss.C4
+    a = ss.synth_problem(C4_SEED, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
+    lo, hi = sn.shard_range(a.N, world, rank)
+    local_arrays = a.slice(lo, hi)
+    solver = sn.Solver(device=local)
+    uid = [sn.unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    solver.dist_init(uid[0], rank, world)
+    shard = sn.DeviceShard(local_arrays, f"cuda:{local}")
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(max(1, args.warmup)):
+        r = solver.dist_solve_dev(shard, lo, a.N)
+    steps = max(1, args.c4_steps)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = solver.dist_solve_dev(shard, lo, a.N)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    plan = shard.plan.cpu().numpy()
+    counts = shard.planned.cpu().numpy()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        parts = [None] * world
+        dist.all_gather_object(parts, (plan.tobytes(), counts.tobytes()))
+    else:
+        parts = [(plan.tobytes(), counts.tobytes())]
+    solver.close()
+    if rank != 0:
+        return None
+    plan_sha = hashlib.sha256(b"".join(p[0] for p in parts)).hexdigest()[:32]
+    counts_sha = hashlib.sha256(b"".join(p[1] for p in parts)).hexdigest()[:32]
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))
+    ok = (gold["plan_sha"] == plan_sha and gold["counts_sha"] == counts_sha and
+          gold["objective_hex"] == float(r["objective"]).hex() and gold["seed"] == C4_SEED)
+    if not ok:
+        raise AssertionError(f"C4 sharded solve differs from the committed twin digest at N={world}")
+    return {
+        "metric": "Shockwave plan solves/sec, one 10k jobs x 30 rounds instance sharded over N GPUs",
+        "value": steps / elapsed,
+        "unit": "plan-solves/s",
+        "ms_per_solve": elapsed / steps * 1e3,
+        "steps": steps,
+        "scaling": "strong",
+        "config": {"workload": f"C4: {a.N} jobs x {a.T} rounds, G={a.G}, k={a.k:g}, "
+                               f"lambda={c['lam']:g}; jobs split over {world} ranks, RCCL",
+                   "jobs": a.N, "rounds": a.T, "ranks": world},
+        "collective_steps": r["iters"],
+        "matches_twin_digest": ok,
+    }
+
 
 
 if __name__ == "__main__":

@@ -86,8 +86,15 @@ def _lp_status(res):
     )
 
 
-def build_p1(prob: Problem):
-    """Assemble P1 exactly as shockwave.py:330-379 (SOS2 formulation of :162-179)."""
+def build_p1(prob: Problem, utility_weight=1.0, makespan_weight=None, makespan_cap=None):
+    """Assemble P1 exactly as shockwave.py:330-379 (SOS2 formulation of :162-179).
+
+    The defaults give the reference model.  The stage problems of the
+    utility-term parity checks reuse the same rows:
+    ``utility_weight=0, makespan_weight=1`` minimises the makespan alone;
+    ``makespan_weight=0, makespan_cap=M`` maximises the utility term with every
+    job's makespan ≤ M.
+    """
     N, T, B = prob.N, prob.T, len(prob.bases)
     ell = log_bases(prob.bases)
     beta = list(prob.bases)
@@ -111,12 +118,14 @@ def build_p1(prob: Problem):
     ub[oz:oz + nz] = 1
     ub[oa:oa + na] = 1
     lb[oM] = -np.inf
+    if makespan_cap is not None:
+        ub[oM] = float(makespan_cap)
     NT = float(N * T)
     for j in range(N):
         for b in range(B):
             # minimise −(p_j ℓ_b / (N·T)) ω_jb
-            c[ow + j * B + b] = -(prob.p[j] * ell[b]) / NT
-    c[oM] = prob.k
+            c[ow + j * B + b] = -utility_weight * (prob.p[j] * ell[b]) / NT
+    c[oM] = prob.k if makespan_weight is None else float(makespan_weight)
     rows, cols, vals, rlo, rhi = [], [], [], [], []
     r = 0
 
@@ -168,8 +177,12 @@ def build_p1(prob: Problem):
     return c, integ, (lb, ub), LinearConstraint(A, np.array(rlo), np.array(rhi)), layout
 
 
-def solve_p1(prob: Problem, rel_gap=1e-3, time_limit=15.0, relax=False):
-    c, integ, (lb, ub), cons, lay = build_p1(prob)
+def solve_p1(prob: Problem, rel_gap=1e-3, time_limit=15.0, relax=False, **variant):
+    """P1 (shockwave.py:330-382) with HiGHS; ``variant`` as build_p1.  Returns
+    (status, x values, objective, dual bound, seconds) in the maximisation
+    sense of the built objective; relax=True solves the LP relaxation (every
+    binary in [0, 1]), whose optimum is an upper bound of the MILP."""
+    c, integ, (lb, ub), cons, lay = build_p1(prob, **variant)
     from scipy.optimize import Bounds
 
     opts = {"disp": False, "time_limit": float(time_limit)}

@@ -162,6 +162,13 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
     /* wait for any run still using the buffers */
     SW_HIP(h, hipStreamSynchronize(h->stream));
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
+    /* the previous batch is gone from here on: a reserve below frees the
+     * old buffers before it allocates, so a failure must leave no batch
+     * described that run / download could touch */
+    h->loaded = false;
+    h->count = 0;
+    h->total_jobs = 0;
+    h->total_plan = 0;
     const size_t Jz = (size_t)std::max<int64_t>(J, 1);
     if (h->d_inst.reserve(std::max(count, 1)) || h->d_out.reserve(std::max(count, 1)) ||
         h->d_w.reserve(Jz) || h->d_F.reserve(Jz) || h->d_E.reserve(Jz) ||
@@ -214,9 +221,6 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         jo += pr.num_jobs;
         po += (int64_t)pr.num_jobs * pr.future_rounds;
     }
-    h->count = count;
-    h->total_jobs = J;
-    h->total_plan = P;
     h->maxN = maxN;
     h->maxT = maxT;
     if (count > 0) {
@@ -233,6 +237,10 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         }
         SW_HIP(h, hipStreamSynchronize(s));
     }
+    h->count = count;
+    h->total_jobs = J;
+    h->total_plan = P;
+    h->loaded = true;
 #ifdef SW_STAMPS
     if (h->d_stamps.reserve((size_t)std::max(count, 1) * 16))
         return fail(h, SW_ERR_HIP, "stamp buffer allocation failed");
@@ -253,6 +261,7 @@ int sw_debug_stamps(sw_handle* h, uint64_t* out) {
 
 int sw_batch_run(sw_handle* h) {
     if (!h) return SW_ERR_INVALID;
+    if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
     if (h->count <= 0) return SW_OK;
     SW_HIP(h, hipSetDevice(h->device));
     sw_batch_dev B;
@@ -296,6 +305,8 @@ int sw_batch_run(sw_handle* h) {
 
 int sw_batch_download(sw_handle* h, sw_result* res) {
     if (!h) return SW_ERR_INVALID;
+    if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
+    if (h->count > 0 && !res) return fail(h, SW_ERR_INVALID, "null result array");
     SW_HIP(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
     if (h->count > 0) {

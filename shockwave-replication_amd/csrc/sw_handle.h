@@ -63,6 +63,7 @@ struct sw_handle {
     bool own_stream = false;
     std::string err;
     /* batch description (host) */
+    bool loaded = false; /* a batch upload completed (run / download need one) */
     int32_t count = 0;
     int64_t total_jobs = 0;
     int64_t total_plan = 0;

@@ -1,7 +1,8 @@
 /*
  * sw_kernels.hip — the MI355X (gfx950) plan-solve kernel.
  *
- * One 1024-thread workgroup (16 wave64) solves one instance end to end:
+ * One 512-thread workgroup (8 wave64, SW_BLOCK in sw_block.h) solves one
+ * instance end to end:
  *   setup     per-job constants and fp32 ranking-key rows — the fused
  *             log-utility-gradient × fairness-weight step — and A = max_j a_j
  *   P1        level search over the makespan M; at each level a price
@@ -15,15 +16,15 @@
  * functions below name the twin function they mirror.  DESIGN.md §3
  * describes the algorithm, §4 the mapping onto CDNA4.
  *
- * Mapping.  N ≤ 1024 (every reference configuration): one job per thread,
- * the job's fp32 key row in VGPRs, per-job state in LDS, every block
+ * Mapping.  N ≤ 1024 (every reference configuration): two jobs per thread
+ * (SW_JPT), their fp32 key rows in VGPRs, per-job state in LDS, every block
  * reduction one barrier (sw_block.h).  Packing sorts the jobs with a
- * register bitonic sort (shuffles for strides < 64, LDS beyond), then ONE
- * wavefront runs the sequential round loop with wave-level scans and ballots
- * over LDS-resident position state — no block barriers inside the loop.
+ * register bitonic sort (shuffles for strides < 128, LDS beyond), then the
+ * whole block runs the round loop of sw_pack.h: each thread keeps its two
+ * sorted positions in VGPRs, tiers and fills are block scans.
  * N > 1024 (the 10k-job C4 shape): several jobs per thread, per-job state
  * and key rows in an HBM workspace (L2-resident), sort through the
- * workspace.
+ * workspace, and wave 0 runs the round loop over workspace position state.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>

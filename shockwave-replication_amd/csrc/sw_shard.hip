@@ -752,7 +752,11 @@ int host_fail(sw_shard_state* S, const char* what) {
 int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
     hipStream_t st = S->h->stream;
     const size_t bytes = (size_t)n * 8;
-    if (S->comm && S->world > 1) { /* one rank: the reduction is the identity */
+    /* with a communicator the all-reduce always runs through RCCL, world 1
+     * included (it is the identity there, but the path is the one the
+     * multi-GPU solve takes); without one (a single rank never initialised
+     * for collectives) it is skipped */
+    if (S->comm) {
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
@@ -774,9 +778,10 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
     hipStream_t st = S->h->stream;
     const size_t total = bytes * (size_t)S->world;
     if (!S->host_comm) {
-        const bool one = !S->comm || S->world == 1;
-        /* one rank: the gather is the identity; a gather read back by the host
-         * is not needed on the device afterwards, so it is copied down directly */
+        const bool one = !S->comm;
+        /* no communicator: the gather is the identity; a gather read back by
+         * the host is not needed on the device afterwards, so it is copied
+         * down directly */
         if (one) {
             if (drecv != dsend && !hrecv)
                 SH_HIP(S, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, st));
@@ -919,7 +924,7 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
                    dim3(kTB), 0, st, S->dv, sr);
         else
             LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, sr);
-        if (S->comm && S->world > 1)
+        if (S->comm)
             SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
                                      S->comm, st));
         LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, S->dv.red);

@@ -4,7 +4,12 @@
  * The reference has no explicit checks; these reject inputs for which its
  * model is undefined or numerically meaningless:
  *   - T < 1 or > SW_MAX_ROUNDS, fewer than 2 bases, bases not increasing
- *     (the SOS2 interpolation of shockwave.py:162-179 needs an ordered grid);
+ *     (the SOS2 interpolation of shockwave.py:162-179 needs an ordered grid),
+ *     or a grid that does not span [0, 1]: the model's progress
+ *     u = (F + e)/E starts at F/E ≥ 0 and Σ ω β = u with Σ ω = 1 caps it at
+ *     the last base, so the per-job reduction (e ≤ E − F, sw_arith.h) holds
+ *     exactly when bases[0] = 0 (log(0) is replaced by log(1e-6),
+ *     shockwave.py:102-103; a negative base has no log) and the last is 1;
  *   - Δ ≤ 0, k < 0 (k < 0 makes the reference's max-makespan term unbounded);
  *   - w < 1, E < 1, F ∉ [0, E] (job_metadata.py:75-78 asserts F ≤ E),
  *     d ≤ 0, non-finite R or priority < 0 (FTF^λ ≥ 0, shockwave.py:368);
@@ -31,6 +36,7 @@ static inline int sw_validate_problem(const sw_problem* pr) {
         if (!sw_finite(pr->log_bases[b]) || !sw_finite(pr->bases[b])) return -1;
         if (b > 0 && !(pr->bases[b] > pr->bases[b - 1])) return -1;
     }
+    if (pr->bases[0] != 0.0 || pr->bases[pr->num_bases - 1] != 1.0) return -1;
     if (pr->num_jobs > 0 && (!pr->nworkers || !pr->epoch_duration || !pr->completed_epochs ||
                              !pr->total_epochs || !pr->remaining_runtime || !pr->priority))
         return -1;

@@ -132,7 +132,28 @@ def test_finished_job_and_zero_priority(twin):
     dict(epoch_duration=[0.0, 1.0]), dict(priority=[-1.0, 1.0]),
     dict(priority=[float("nan"), 1.0]), dict(regularizer=-1.0), dict(future_rounds=65),
     dict(nworkers=[256, 1], num_gpus=300),  # schedulable but wider than SW_MAX_WIDTH
+    dict(bases=(0.1, 0.5, 1.0)),  # grid must start at 0 (u = F/E can be 0)
+    dict(bases=(0.0, 0.5, 0.9)),  # and end at 1 (Σωβ caps progress at the last base)
+    dict(bases=(0.0, 0.5, 0.5, 1.0)),  # strictly increasing
 ])
 def test_invalid_inputs_rejected(bad, twin):
     a = _arr(**bad)
     assert twin.rc(a) == sn.SW_ERR_INVALID
+
+
+NONDEFAULT_BASES = [(0.0, 0.1, 0.5, 1.0), (0.0, 0.05, 0.15, 0.3, 0.5, 0.7, 0.85, 1.0), (0.0, 1.0)]
+
+
+@pytest.mark.parametrize("bases", NONDEFAULT_BASES, ids=lambda b: f"nb{len(b)}")
+def test_twin_nondefault_bases_vs_reference_milp(bases, twin):
+    """log_approximation_bases other than the JSONs' six (shockwave.py:99-105,
+    :162-181): the PWL utility, slopes and caps follow the grid."""
+    a = ss.synth_problem(31, 60, 32, 12, 120.0, 1e-3, 15.0, bases=bases)
+    P = to_oracle(a)
+    sol = mr.plan_solve(P, rel_gap=1e-5, time_limit=60)
+    ref = mr.evaluate_counts(P, sol.n)[0]
+    r = twin.solve(a)
+    check_plan_valid(a, r)
+    got, util, mk = mr.evaluate_counts(P, r["planned_rounds"])
+    assert got >= ref - REL_TOL * abs(ref), (got, ref)
+    assert math.isclose(r["utility"], util, rel_tol=1e-9, abs_tol=1e-12)

@@ -1,0 +1,111 @@
+"""Headline-size parity against the ORACLE (oracle/milp_ref.py), not the twin.
+
+tests/golden/oracle_c3.json (tests/golden/make_oracle_c3.py) holds, for 8 C3
+instances (900 jobs x 30 rounds, G=256, k=1e5, lambda=5 — the bench's
+configuration) and 8 C5-mix instances (G in {32, 64, 128, 256} with the
+matching scale_*gpus.json k / lambda), the reference model solved by HiGHS:
+the P1 MILP objective J_ref (shockwave.py:330-382, gap 1e-4), its LP
+relaxation bound, the smallest makespan M*, the utility term's optimum U* at
+that makespan (at k >= 10 the k*M term swamps a
+relative check of J, so the utility term is checked on its own), and the P2
+MILP optimum (shockwave.py:281-328) for the solver's planned counts.
+
+Bars (one-sided, BASELINE.json north star: within 1e-3 relative):
+  * J >= J_ref - 1e-3 |J_ref|, and J <= the MILP's certified dual bound;
+  * (J_lp - J) / |J| <= 1e-3: the LP relaxation bound certifies J;
+  * when k >= 1 (makespan-dominated): M == M* and U >= U* - 1e-3 |U*|,
+    U <= the certified dual bound of the utility problem;
+  * P2 objective <= P2_MILP * (1 + 2e-3) (the reference solves P2 at gap 1e-3).
+
+The CPU test runs the twin (same algorithm, bit-exact with the GPU); the GPU
+test solves all 16 instances in ONE batched launch of the HIP kernel and
+applies the same bars to the GPU's own plans and objectives.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import milp_ref as mr
+import sw_synth as ss
+from helpers import check_plan_valid, to_oracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_c3.json")
+REL = 1e-3
+P2_TOL = 2e-3
+
+
+def _cases():
+    if not os.path.exists(GOLD):
+        return []
+    return json.load(open(GOLD))["cases"]
+
+
+CASES = _cases()
+IDS = [f"{c['name']}_s{c['seed']}_G{c['G']}" for c in CASES]
+
+
+def problem(c):
+    cfg = ss.CLUSTER_CONFIG[c["G"]]
+    a = ss.synth_problem(c["seed"], c["N"], c["G"], c["T"], 120.0, cfg["k"], cfg["lam"])
+    h = hashlib.sha256()
+    for arr in (a.w, a.d, a.F, a.E, a.R, a.p):
+        h.update(np.ascontiguousarray(arr).tobytes())
+    assert h.hexdigest()[:32] == c["inputs_sha"], "synthetic inputs changed: regenerate the fixture"
+    return a
+
+
+def check_against_oracle(c, a, r):
+    """The one-sided oracle bars on one solver result r (plan, counts, J, U, M)."""
+    check_plan_valid(a, r)
+    P = to_oracle(a)
+    J, U, M = mr.evaluate_counts(P, r["planned_rounds"])  # independent closed form (milp_ref)
+    assert np.isclose(J, r["objective"], rtol=1e-9, atol=1e-9), (J, r["objective"])
+    assert np.isclose(U, r["utility"], rtol=1e-9, atol=1e-12), (U, r["utility"])
+    Jr = c["p1"]["J"]
+    assert J >= Jr - REL * abs(Jr), ("objective below the reference MILP", J, Jr)
+    assert J <= c["p1"]["dual_bound"] + 1e-9 * abs(c["p1"]["dual_bound"]), "beats a certified bound"
+    assert (c["p1_lp"]["bound"] - J) / abs(J) <= REL, ("LP bound does not certify J",
+                                                      c["p1_lp"]["bound"], J)
+    if c["k"] >= 1.0:
+        Ms, Us = c["mk_min"]["M"], c["util_at"]["U"]
+        assert M <= Ms * (1 + 1e-12), ("makespan above the smallest feasible", M, Ms)
+        assert U >= Us - REL * abs(Us), ("utility term below the oracle at M*", U, Us)
+        ub = c["util_at"]["dual_bound"]
+        assert U <= ub + 1e-9 * abs(ub), ("utility beats a certified bound", U, ub)
+    counts = np.ascontiguousarray(r["planned_rounds"], dtype=np.int32)
+    if hashlib.sha256(counts.tobytes()).hexdigest()[:32] == c["p2"]["counts_sha"]:
+        p2 = mr.p2_objective(P, r["plan"])
+        assert p2 <= c["p2"]["objective"] * (1 + P2_TOL) + 1e-9, ("P2 above the MILP",
+                                                                  p2 / c["p2"]["objective"])
+    else:
+        pytest.fail("planned counts differ from the fixture's: regenerate tests/golden/oracle_c3.json")
+    return J, U, M
+
+
+def test_fixture_present_and_complete():
+    assert len(CASES) == 16, "tests/golden/oracle_c3.json: run tests/golden/make_oracle_c3.py"
+    assert sum(c["name"] == "c3" for c in CASES) == 8
+    assert sorted({c["G"] for c in CASES if c["name"] == "c5"}) == [32, 64, 128, 256]
+    for c in CASES:
+        assert c["p1"]["feasible"] and c["p1"]["status"] in ("optimal", "time_limit")
+        assert c["mk_min"]["lower_bound"] <= c["mk_min"]["M"] * (1 + 1e-9)
+
+
+@pytest.mark.parametrize("i", range(len(CASES)), ids=IDS)
+def test_twin_vs_oracle_headline(i, twin):
+    c = CASES[i]
+    a = problem(c)
+    check_against_oracle(c, a, twin.solve(a))
+
+
+@pytest.mark.gpu
+def test_gpu_vs_oracle_headline_one_launch(gpu_solver):
+    """All 16 headline-size instances in ONE batched launch of sw_plan_kernel
+    (C3 and the C5 G-mix), each held to the oracle bars above."""
+    probs = [problem(c) for c in CASES]
+    rs = gpu_solver.solve_batch(probs)
+    for c, a, r in zip(CASES, probs, rs):
+        check_against_oracle(c, a, r)

@@ -2,7 +2,8 @@
 (shockwave.py:12-91, :224-279, :390-398) with the solve injected.
 
 On CPU the product path has no solver (no GPU, no fallback), so these tests
-inject the CPU twin explicitly; the GPU versions live in test_gpu_scheduler.py.
+inject the CPU twin explicitly; the scheduler on the HIP solver is exercised
+on the GPU by test_gpu_sim.py (whole simulations through ShockwaveScheduler).
 """
 import copy
 import random
