@@ -59,6 +59,7 @@ extern "C" {
  * density order p_j/(n_j·w_j) placed every round. */
 #define SW_STATUS_P2_WEIGHT_ORDER 0x8 /* the weight order p_j/n_j placed every round   */
 #define SW_STATUS_P2_CLASSWISE 0x10   /* width classes repacked inside the P1 profile  */
+#define SW_STATUS_P2_REPAIRED 0x20    /* density order with its width profile repaired */
 
 /*
  * One plan solve.  Field ↔ reference:

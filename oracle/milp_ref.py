@@ -307,20 +307,31 @@ class MilpSolver:
     read-back, shockwave.py:330-411) with HiGHS in place of Gurobi.  Used by
     the simulator-parity tests and tools/sim_parity.py as the oracle run."""
 
-    def __init__(self, rel_gap=1e-3, time_limit=15.0):
+    def __init__(self, rel_gap=1e-3, time_limit=15.0, perm_seed=None):
+        """perm_seed: solve every model with its jobs in a seeded random order
+        (the same problem; HiGHS then walks a different path and may stop at a
+        different solution inside the gap) — samples the oracle's own
+        indeterminacy at a given gap."""
         self.rel_gap = rel_gap
         self.time_limit = time_limit
+        self.perm_seed = perm_seed
         self.seconds = 0.0
         self.calls = 0
 
     def solve(self, arrays):
-        prob = Problem(arrays.w, arrays.d, arrays.F, arrays.E, arrays.R, arrays.p, arrays.T,
-                       arrays.G, arrays.delta, arrays.k, list(arrays.bases))
+        perm = np.arange(arrays.N)
+        if self.perm_seed is not None:
+            perm = np.random.default_rng([self.perm_seed, self.calls]).permutation(arrays.N)
+        prob = Problem(arrays.w[perm], arrays.d[perm], arrays.F[perm], arrays.E[perm],
+                       arrays.R[perm], arrays.p[perm], arrays.T, arrays.G, arrays.delta,
+                       arrays.k, list(arrays.bases))
         t0 = time.perf_counter()
         sol = plan_solve(prob, self.rel_gap, self.time_limit)
         self.seconds += time.perf_counter() - t0
         self.calls += 1
-        y = sol.y.astype(np.uint8)
+        y = np.empty_like(sol.y)
+        y[perm] = sol.y
+        y = y.astype(np.uint8)
         return {"rc": 0 if sol.p2_status in ("optimal", "no_planned", "time_limit") else 1,
                 "plan": y, "planned_rounds": y.sum(axis=1).astype(np.int32),
                 "objective": sol.objective, "utility": float("nan"), "makespan": float("nan"),

@@ -28,6 +28,7 @@
 
 #include "../include/shockwave_amd.h"
 #include "../shockwave-replication_amd/csrc/sw_arith.h"
+#include "../shockwave-replication_amd/csrc/sw_repair.h"
 #include "../shockwave-replication_amd/csrc/sw_validate.h"
 
 typedef struct {
@@ -332,6 +333,57 @@ static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const 
     free(ord); free(r); free(ww); free(sel);
 }
 
+/* Density placement with profile repair (sw_repair.h): yd / pd are the
+ * density-order pack of nin that left rounds unplaced.  Builds the width
+ * classes' profile and free GPUs per round from it, repairs the profile and
+ * repacks every changed class alone (unit widths, order p_j/n_j) inside its
+ * new capacities; unchanged classes keep their density rows.  Writes yout
+ * and placed; returns 1 when every round of nin is placed. */
+static int repair_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin, const uint8_t* yd,
+                       const int32_t* pd, uint8_t* yout, int32_t* placed) {
+    const int32_t N = P->N, T = P->T;
+    sw_repair_t R;
+    memset(&R, 0, sizeof(R));
+    for (int32_t j = 0; j < N; ++j)
+        if (nin[j] > 0 && sw_repair_add_class(&R, P->jc[j].w) < 0) return 0;
+    for (int32_t t = 0; t < T; ++t) R.L[t] = P->G;
+    for (int32_t j = 0; j < N; ++j) {
+        for (int32_t t = 0; t < T; ++t) R.L[t] -= P->jc[j].w * yd[(size_t)j * T + t];
+        if (nin[j] <= 0) continue;
+        const int32_t c = sw_repair_class(&R, P->jc[j].w);
+        R.M[c] += 1;
+        R.D[c] += nin[j] - pd[j];
+        for (int32_t t = 0; t < T; ++t) R.caps[c][t] += yd[(size_t)j * T + t];
+    }
+    if (sw_profile_repair(&R, T) != 0) return 0;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    memcpy(yout, yd, NN * (size_t)T);
+    memcpy(placed, pd, sizeof(int32_t) * NN);
+    int32_t* nc = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
+    uint32_t* k2 = (uint32_t*)calloc(NN, sizeof(uint32_t));
+    uint8_t* yc = (uint8_t*)malloc(NN * (size_t)(T > 0 ? T : 1));
+    for (int32_t c = 0; c < R.ncls; ++c) {
+        if (!R.changed[c]) continue;
+        for (int32_t j = 0; j < N; ++j) {
+            const int cls = nin[j] > 0 && P->jc[j].w == R.wc[c];
+            nc[j] = cls ? nin[j] : 0;
+            k1[j] = cls ? sw_bits(pr->priority[j] / (double)nin[j]) : 0;
+        }
+        pack(P, nc, k1, k2, yc, pc, R.caps[c], 1);
+        for (int32_t j = 0; j < N; ++j)
+            if (nc[j] > 0) {
+                memcpy(yout + (size_t)j * T, yc + (size_t)j * T, (size_t)T);
+                placed[j] = pc[j];
+            }
+    }
+    int ok = 1;
+    for (int32_t j = 0; j < N; ++j) ok &= (placed[j] == nin[j]);
+    free(nc); free(pc); free(k1); free(k2); free(yc);
+    return ok;
+}
+
 /* The packer over plain arrays, for the sharded CPU engine (oracle/shard_twin.c):
  * pack() reads only N, T, G and the widths. */
 void twin_pack_arrays_caps(int32_t N, int32_t T, int32_t G, const int32_t* w, const int32_t* nin,
@@ -499,6 +551,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     int32_t* nbest = (int32_t*)malloc(sizeof(int32_t) * NN);
     double bound = 0.0, Jbest = 0.0;
     int dens_best = 0; /* the best P1 plan is the density-order pack */
+    int rep_best = 0;  /* ... with its width profile repaired (sw_repair.h) */
     int dskip_best = 0; /* density failed on exactly the final counts: P2 (a) would too */
     for (int it = 0; it < SW_REPACK_ITERS; ++it) {
         double b0 = level_search(&P, n, nb, l, tk, tmp);
@@ -513,7 +566,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
          * k > 0).  Keep the better packed plan of A and B. */
         int64_t deficit = 0;
         double Jp = 0.0;
-        int dens = 0;
+        int dens = 0, rep = 0;
         for (int ord = -1; ord < 2; ++ord) {
             for (int32_t j = 0; j < N; ++j) {
                 if (ord < 0) {
@@ -540,6 +593,22 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
             double Jo = sw_detsum(tmp, N) - P.k * Mp;
             P.passes++;
             if (ord < 0) {
+                /* the density pack stranded rounds: repair its width profile
+                 * (sw_repair.h); a repaired placement places every count and
+                 * is also the P2 placement, like a density pack that fits */
+                if (dfc != 0 && repair_pack(&P, pr, nb, y1, placed, y2, placed2)) {
+                    memcpy(y1, y2, NN * (size_t)T);
+                    memcpy(placed, placed2, sizeof(int32_t) * NN);
+                    dfc = 0;
+                    rep = 1;
+                    Mp = 0.0;
+                    for (int32_t j = 0; j < N; ++j) {
+                        tmp[j] = fval(&P, j, placed[j]);
+                        Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
+                    }
+                    Jo = sw_detsum(tmp, N) - P.k * Mp;
+                    P.passes++;
+                }
                 if (dfc == 0) { Jp = Jo; dens = 1; break; }
                 continue;
             }
@@ -556,6 +625,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             dens_best = dens;
+            rep_best = rep;
             dskip_best = !dens && deficit == 0;
             memcpy(nbest, placed, sizeof(int32_t) * NN);
             memcpy(ybest, y1, NN * (size_t)T);
@@ -580,6 +650,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     if (dens_best) { /* (a) is the P1 placement itself */
         memcpy(y2, y1, NN * (size_t)T);
         ok2 = 1;
+        if (rep_best) status |= SW_STATUS_P2_REPAIRED;
     }
     for (int att = 0; att < 2 && !ok2; ++att) {
         if (att == 0 && dskip_best) continue;
@@ -592,6 +663,15 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         pack(&P, nb, k1, k2, y2, placed, NULL, 0);
         ok2 = 1;
         for (int32_t j = 0; j < N; ++j) ok2 &= (placed[j] == nb[j]);
+        if (!ok2 && att == 0) { /* (a') density with its profile repaired */
+            uint8_t* yr = (uint8_t*)malloc(NN * (size_t)T);
+            ok2 = repair_pack(&P, pr, nb, y2, placed, yr, placed2);
+            if (ok2) {
+                memcpy(y2, yr, NN * (size_t)T);
+                status |= SW_STATUS_P2_REPAIRED;
+            }
+            free(yr);
+        }
         if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
     }
     if (!ok2) {

@@ -254,6 +254,8 @@ static int e_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* l
             s += (int64_t)c->w * (E->arr[SW_A_NB][i] - pl);
         } else if (sel == SW_EV_P2OK) {
             s += E->arr[SW_A_PL][i] != E->arr[SW_A_NFIN][i];
+        } else if (sel == SW_EV_UNPLACED) {
+            s += E->arr[arg & 0xFF][i] != E->arr[arg >> 8][i];
         } else { /* SW_EV_FINAL */
             const uint64_t m = E->y[arg][i];
             int32_t cn = 0;
@@ -362,26 +364,31 @@ static int e_pack_class(void* ctx, int32_t src, int32_t wc, const int32_t* caps,
     return e_pack_any((eng_t*)ctx, 5, src, 0.0, ydst, pdst, wc, caps);
 }
 
-static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps,
-                        int32_t* next_w) {
+static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc,
+                        int32_t* caps, int32_t* next_w, int64_t* md) {
     eng_t* E = (eng_t*)ctx;
-    int64_t buf[SW_TMAX];
+    int64_t buf[SW_TMAX + 2];
     uint64_t nx = 0; /* max of ~next: the min width above wc */
-    for (int32_t t = 0; t < E->T; ++t) buf[t] = 0;
+    for (int32_t t = 0; t < E->T + 2; ++t) buf[t] = 0;
     for (int32_t i = 0; i < E->NL; ++i) {
         if (E->arr[src][i] <= 0) continue;
         const int32_t w = E->jc[i].w;
-        if (w == wc)
+        if (w == wc) {
             for (int32_t t = 0; t < E->T; ++t) buf[t] += (int64_t)((E->y[ysrc][i] >> t) & 1u);
+            buf[E->T] += 1;
+            if (psrc >= 0) buf[E->T + 1] += E->arr[src][i] - E->arr[psrc][i];
+        }
         if (w > wc) {
             const uint64_t v = 0xFFFFFFFFull - (uint64_t)w;
             nx = v > nx ? v : nx;
         }
     }
-    int rc = E->comm->allreduce_sum_i64(E->comm->ctx, buf, E->T);
+    int rc = E->comm->allreduce_sum_i64(E->comm->ctx, buf, E->T + 2);
     if (!rc) rc = E->comm->allreduce_max_u64(E->comm->ctx, &nx, 1);
     if (rc) return -1;
     for (int32_t t = 0; t < E->T; ++t) caps[t] = (int32_t)buf[t];
+    md[0] = buf[E->T];
+    md[1] = buf[E->T + 1];
     *next_w = nx == 0 ? 0x7FFFFFFF : (int32_t)(0xFFFFFFFFull - nx);
     return 0;
 }

@@ -34,6 +34,7 @@
 #include "sw_block.h"
 #include "sw_device.h"
 #include "sw_pack.h"
+#include "sw_repair.h"
 
 namespace {
 
@@ -98,6 +99,7 @@ struct Ctx {
     int32_t pwc;
     int32_t* caps;
     int64_t* misc;
+    sw_repair_t* rep; /* LDS: the width profile of repair_pack */
     /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
     sw_jobc jcs[SW_JPT];
     float kr[SW_JPT][KT];
@@ -831,6 +833,84 @@ struct Ctx {
         }
     }
 
+    /*
+     * twin: repair_pack — yd / pd are the density-order pack of nin that left
+     * rounds unplaced.  The width classes' profile and the free GPUs per
+     * round are gathered from it (LDS atomics), one thread repairs the
+     * profile (sw_repair.h), and every changed class is repacked alone
+     * (pack mode 5, unit widths, order p_j/n_j) inside its new capacities
+     * into yout / pout; unchanged classes keep their density rows.  True
+     * when every round of nin is placed.
+     */
+    __device__ __forceinline__ bool repair_pack(const uint8_t* nin, const uint64_t* yd,
+                                                const uint8_t* pd, uint64_t* yout, uint8_t* pout) {
+        sw_repair_t* R = rep;
+        uint32_t* wset = reinterpret_cast<uint32_t*>(misc); /* widths present: 256 bits */
+        int32_t* flag = reinterpret_cast<int32_t*>(misc) + 8;
+        __syncthreads(); /* earlier users of caps / misc are done */
+        for (int i = threadIdx.x; i < (int)(sizeof(sw_repair_t) / 4); i += SW_BLOCK)
+            reinterpret_cast<int32_t*>(R)[i] = 0;
+        if (threadIdx.x < 8) wset[threadIdx.x] = 0;
+        __syncthreads();
+        for_jobs([&](int j, int s) {
+            (void)s;
+            if (nin[j] > 0) atomicOr(&wset[(w_in[j] >> 5) & 7], 1u << (w_in[j] & 31));
+        });
+        if (threadIdx.x < T) R->L[threadIdx.x] = G;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int32_t n = 0;
+            for (int wd = 0; wd < 8; ++wd) {
+                uint32_t m = wset[wd];
+                while (m) {
+                    const int b = __builtin_ctz(m);
+                    m &= m - 1u;
+                    if (n < SW_RCLS_MAX) R->wc[n] = wd * 32 + b;
+                    ++n;
+                }
+            }
+            R->ncls = n;
+        }
+        __syncthreads();
+        if (R->ncls > SW_RCLS_MAX) return false; /* uniform */
+        for_jobs([&](int j, int s) {
+            (void)s;
+            const uint64_t m = yd[j];
+            const int32_t w = w_in[j];
+            for (int t = 0; t < T; ++t)
+                if ((m >> t) & 1ull) atomicSub(&R->L[t], w);
+            if (nin[j] > 0) {
+                const int32_t c = sw_repair_class(R, w);
+                atomicAdd(&R->M[c], 1);
+                atomicAdd(&R->D[c], (int32_t)nin[j] - (int32_t)pd[j]);
+                for (int t = 0; t < T; ++t)
+                    if ((m >> t) & 1ull) atomicAdd(&R->caps[c][t], 1);
+            }
+        });
+        __syncthreads();
+        if (threadIdx.x == 0) flag[0] = sw_profile_repair(R, T);
+        __syncthreads();
+        if (flag[0] != 0) return false; /* uniform */
+        for_jobs([&](int j, int s) {
+            (void)s;
+            yout[j] = yd[j];
+            pout[j] = pd[j];
+        });
+        for (int ci = 0; ci < R->ncls; ++ci) {
+            if (!R->changed[ci]) continue;
+            __syncthreads(); /* the previous class's pack has read caps */
+            if (threadIdx.x < 64) caps[threadIdx.x] = threadIdx.x < T ? R->caps[ci][threadIdx.x] : 0;
+            pwc = R->wc[ci];
+            pack(5, nin, yout, pout);
+        }
+        int64_t bad = 0;
+        for_jobs([&](int j, int s) {
+            (void)s;
+            bad += pout[j] != nin[j];
+        });
+        return blk.sum(bad) == 0;
+    }
+
     /* The round loop of pack, run by wave 0 alone (twin: the t loop of
      * pack).  Lane L owns positions [L·PPL, L·PPL + PPL) (prefix order =
      * lane-major); their state lives at tslot(p). */
@@ -958,7 +1038,7 @@ struct Ctx {
 __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     size_t s = r16(sizeof(sw_xchg)) + r16(sizeof(double) * 3 * SW_BMAX) +
-               r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8);
+               r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) + r16(sizeof(sw_repair_t));
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
         s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
@@ -1010,6 +1090,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.caps = c.PL->H[1]; /* spare row of the pack LDS */
     c.pwc = 0;
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
+    c.rep = (sw_repair_t*)carve(sizeof(sw_repair_t));
     if (threadIdx.x < SW_BMAX) {
         const int b = (int)threadIdx.x;
         bt[b] = I->beta[b];
@@ -1087,6 +1168,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     int it = 0, mode = 0; /* mode 0 = run the level search next */
     bool ok2 = true;
     bool dens = false, dens_best = false; /* P1 placed by the density order */
+    bool rep = false, rep_best = false;   /* ... after a width-profile repair */
     bool dskip_best = false; /* density failed on exactly the final counts */
     while (true) {
         if (mode == 0) {
@@ -1095,6 +1177,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             SW_STAMP(1);
             mode = 4; /* P1 orders: density, then A (1), then B (3) */
             dens = false;
+            rep = false;
         }
         if (mode == 2) break; /* P2 below */
         uint8_t* pl = (mode == 3) ? c.placed2 : c.placed;
@@ -1107,12 +1190,28 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             fs = fs + c.fval(j, s, pl[j]);
             gm = sw_max(gm, c.gval(j, s, pl[j]));
         });
-        const int64_t dfc = c.blk.sum(def_l);
+        int64_t dfc = c.blk.sum(def_l);
         double U, Mx;
         c.blk.detsum_max(fs, gm, U, Mx);
-        const double Jo = U - c.k * Mx;
+        double Jo = U - c.k * Mx;
         c.passes++;
         if (mode == 4) { /* density order: also the P2 placement when it packs */
+            /* stranded rounds: repair the width profile (sw_repair.h) */
+            if (dfc != 0 && c.repair_pack(c.nbest, c.ycur, c.placed, c.y2, c.placed2)) {
+                fs = 0.0;
+                gm = 0.0;
+                c.for_jobs([&](int j, int s) {
+                    c.ycur[j] = c.y2[j];
+                    c.placed[j] = c.placed2[j];
+                    fs = fs + c.fval(j, s, c.placed[j]);
+                    gm = sw_max(gm, c.gval(j, s, c.placed[j]));
+                });
+                c.blk.detsum_max(fs, gm, U, Mx);
+                Jo = U - c.k * Mx;
+                c.passes++;
+                dfc = 0;
+                rep = true;
+            }
             if (dfc != 0) { mode = 1; continue; }
             Jp = Jo;
             deficit = 0;
@@ -1134,6 +1233,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;
             dens_best = dens;
+            rep_best = rep;
             dskip_best = !dens && deficit == 0;
             c.for_jobs([&](int j, int s) {
                 (void)s;
@@ -1164,11 +1264,19 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     if (dens_best) { /* (a) is the P1 placement itself */
         c.for_jobs([&](int j, int s) { (void)s; c.y2[j] = c.ybest[j]; });
         ok2 = true;
+        if (rep_best) status |= SW_STATUS_P2_REPAIRED;
     }
     for (int att = 0; att < 2 && !ok2; ++att) {
         if (att == 0 && dskip_best) continue;
         c.pack(att == 0 ? 4 : 2, c.nfin, c.y2, c.placed);
         ok2 = p2_ok();
+        if (!ok2 && att == 0) { /* (a') density with its width profile repaired */
+            ok2 = c.repair_pack(c.nfin, c.y2, c.placed, c.ycur, c.placed2);
+            if (ok2) {
+                c.for_jobs([&](int j, int s) { (void)s; c.y2[j] = c.ycur[j]; });
+                status |= SW_STATUS_P2_REPAIRED;
+            }
+        }
         if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
     }
     if (!ok2) {

@@ -420,7 +420,7 @@ __global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
  * red[0] = max g (bits), red[1] = integer sum.  SW_EV_FINAL also writes the
  * plan row and count of job i. */
 __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const int32_t* arr,
-                                                   const uint64_t* ysrc) {
+                                                   const uint64_t* ysrc, int arr_a, int arr_b) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     double fa = 0.0, fb = 0.0, gm = 0.0;
     long long is = 0;
@@ -440,6 +440,8 @@ __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const in
             is = (long long)c.w * (S.arr[SW_A_NB][i] - pl);
         } else if (sel == SW_EV_P2OK) {
             is = S.arr[SW_A_PL][i] != S.arr[SW_A_NFIN][i];
+        } else if (sel == SW_EV_UNPLACED) {
+            is = S.arr[arr_a][i] != S.arr[arr_b][i];
         } else { /* SW_EV_FINAL */
             const uint64_t m = ysrc[i];
             const int cn = __popcll(m);
@@ -525,19 +527,28 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
     out[i] = e;
 }
 
-/* class-wise P2: red[t] = #{local j : src_j > 0, w_j = wc, bit t of ys_j};
- * red[64] = max over local j with src_j > 0 and w_j > wc of ~w_j */
+/* width-class profile: red[t] = #{local j : src_j > 0, w_j = wc, bit t of
+ * ys_j}; red[64] = max over local j with src_j > 0 and w_j > wc of ~w_j;
+ * red[65] = #{local j : src_j > 0, w_j = wc}, red[66] = Σ over them of
+ * src_j − ps_j (ps = nullptr: 0) */
 __global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* src,
-                                                    const uint64_t* ys, int wc) {
+                                                    const uint64_t* ys, int wc, const int32_t* ps) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     uint64_t m = 0, nx = 0;
+    long long mem = 0, dfc = 0;
     if (i < S.NL && src[i] > 0) {
         const int w = S.jc[i].w;
-        if (w == wc) m = ys[i];
+        if (w == wc) {
+            m = ys[i];
+            mem = 1;
+            dfc = ps ? (long long)(src[i] - ps[i]) : 0;
+        }
         if (w > wc) nx = 0xFFFFFFFFull - (uint64_t)w;
     }
     for (int t = 0; t < S.T; ++t) red_add(S.red + t, (long long)((m >> t) & 1ull));
     red_umax(S.red + 64, nx);
+    red_add(S.red + 65, mem);
+    red_add(S.red + 66, dfc);
 }
 
 /* per-solve state: every count array, every bitmask, l and taken = 0 */
@@ -996,7 +1007,8 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     SH_TRY(zero_red(S, 2));
     const int32_t* arr = sel == SW_EV_GMAX || sel == SW_EV_PACKED ? S->arr[arg].p : nullptr;
     const uint64_t* ys = sel == SW_EV_FINAL ? S->y[arg].p : nullptr;
-    LAUNCH(S, k_eval_jobs, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (int)sel, arr, ys);
+    LAUNCH(S, k_eval_jobs, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (int)sel, arr, ys,
+           (int)(arg & 0xFF), (int)(arg >> 8));
     LAUNCH(S, k_eval_lanes, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, S->xsend.p);
     std::vector<double> all((size_t)blk * S->world);
     SH_TRY(coll_gather(S, S->xsend.p, S->xrecv.p, (size_t)blk * 8, all.data()));
@@ -1080,15 +1092,17 @@ int op_pack_class(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32
     return pack_any((sw_shard_state*)ctx, 5, src, 0.0, ydst, pdst, wc, caps);
 }
 
-int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps, int32_t* next_w) {
+int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc, int32_t* caps,
+                  int32_t* next_w, int64_t* md) {
     auto* S = (sw_shard_state*)ctx;
-    SH_TRY(zero_red(S, 65));
+    SH_TRY(zero_red(S, 67));
     LAUNCH(S, k_class_caps, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p,
-           S->y[ysrc].p, (int)wc);
+           S->y[ysrc].p, (int)wc, psrc >= 0 ? (const int32_t*)S->arr[psrc].p : nullptr);
     int64_t cnt[64];
     uint64_t nx = 0;
     SH_TRY(coll_reduce(S, S->dv.red, S->T, 0, cnt));
     SH_TRY(coll_reduce(S, S->dv.red + 64, 1, 1, &nx));
+    SH_TRY(coll_reduce(S, S->dv.red + 65, 2, 0, md));
     for (int t = 0; t < S->T; ++t) caps[t] = (int32_t)cnt[t];
     *next_w = nx == 0 ? 0x7FFFFFFF : (int32_t)(0xFFFFFFFFull - nx);
     return SW_OK;

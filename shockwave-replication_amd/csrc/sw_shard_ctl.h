@@ -42,6 +42,7 @@
 #include <string.h>
 
 #include "sw_arith.h"
+#include "sw_repair.h"
 
 #define SW_SHARD_K 63 /* thresholds evaluated per search step (≤ 63) */
 
@@ -63,8 +64,9 @@ enum {
     SW_EV_GMAX = 1,   /* gm: g(arr[arg])                                             */
     SW_EV_PACKED = 2, /* A: f(arr[arg])  gm: g(arr[arg])  isum: Σ w·(nb − arr[arg])  */
     SW_EV_P2OK = 3,   /* isum: #{j : placed ≠ nfin}                                  */
-    SW_EV_FINAL = 4   /* y = Y[arg]: c = popcount(y); A: f(c)  B: S(y)/c·p  gm: g(c)
+    SW_EV_FINAL = 4,  /* y = Y[arg]: c = popcount(y); A: f(c)  B: S(y)/c·p  gm: g(c)
                          isum: #{c > 0}; also writes the plan rows and counts        */
+    SW_EV_UNPLACED = 5 /* isum: #{j : arr[arg & 0xFF]_j ≠ arr[arg >> 8]_j}           */
 };
 
 typedef struct sw_shard_ops {
@@ -101,11 +103,14 @@ typedef struct sw_shard_ops {
      * (Mb = makespan of arr[src]), 2 = P2 weight order p/n, 4 = P2 density
      * order p/(n·w).  Writes Y[ydst], arr[pdst] */
     int (*pack)(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst);
-    /* class-wise P2 (twin: the (c) placement).  caps[t] = #{j : arr[src]_j > 0,
-     * w_j = wc, bit t of Y[ysrc]_j} summed over all ranks; next_w = the
-     * smallest width > wc among jobs with arr[src]_j > 0 (0x7FFFFFFF if none) */
-    int (*class_caps)(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t* caps,
-                      int32_t* next_w);
+    /* width-class profile (twin: the (c) placement and repair_pack).
+     * caps[t] = #{j : arr[src]_j > 0, w_j = wc, bit t of Y[ysrc]_j} summed over
+     * all ranks; next_w = the smallest width > wc among jobs with
+     * arr[src]_j > 0 (0x7FFFFFFF if none); with psrc ≥ 0 also md[0] = #{j :
+     * arr[src]_j > 0, w_j = wc} and md[1] = Σ over them of arr[src]_j −
+     * arr[psrc]_j (the class's unplaced rounds) */
+    int (*class_caps)(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc,
+                      int32_t* caps, int32_t* next_w, int64_t* md);
     /* pack the jobs of width wc (arr[src] rounds, order p/n, unit widths) into
      * per-round capacities caps; writes their rows of Y[ydst] and arr[pdst]
      * and leaves every other job untouched */
@@ -331,6 +336,53 @@ static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
     return 0;
 }
 
+/* twin: repair_pack — the density pack (Y[ysrc], arr[psrc]) of arr[nin]
+ * stranded rounds: gather the width-class profile, repair it on the host
+ * (sw_repair.h, identical on every rank), repack every changed class into
+ * Y[ydst] / arr[pdst] (the rest copied from the density pack).  *ok = every
+ * round placed. */
+static inline int swc_repair(sw_shard_ctl* c, int32_t nin, int32_t ysrc, int32_t psrc,
+                             int32_t ydst, int32_t pdst, int* ok) {
+    const sw_shard_ops* o = c->ops;
+    sw_repair_t R;
+    int32_t caps[SW_TMAX];
+    int32_t next_w = 0, wc;
+    int64_t md[2] = {0, 0};
+    int over = 0;
+    memset(&R, 0, sizeof(R));
+    *ok = 0;
+    SWC_TRY(o->class_caps(o->ctx, nin, ysrc, 0, -1, caps, &next_w, md));
+    c->steps++;
+    for (int32_t t = 0; t < c->T; ++t) R.L[t] = c->G;
+    while (next_w != 0x7FFFFFFF) {
+        wc = next_w;
+        SWC_TRY(o->class_caps(o->ctx, nin, ysrc, wc, psrc, caps, &next_w, md));
+        c->steps++;
+        const int32_t ci = sw_repair_add_class(&R, wc);
+        if (ci < 0) { over = 1; continue; }
+        R.M[ci] = (int32_t)md[0];
+        R.D[ci] = (int32_t)md[1];
+        for (int32_t t = 0; t < c->T; ++t) {
+            R.caps[ci][t] = caps[t];
+            R.L[t] -= wc * caps[t];
+        }
+    }
+    if (over || sw_profile_repair(&R, c->T) != 0) return 0;
+    SWC_TRY(o->copy_y(o->ctx, ydst, ysrc));
+    SWC_TRY(o->copy(o->ctx, pdst, psrc));
+    for (int32_t ci = 0; ci < R.ncls; ++ci) {
+        if (!R.changed[ci]) continue;
+        SWC_TRY(o->pack_class(o->ctx, nin, R.wc[ci], R.caps[ci], ydst, pdst));
+        c->steps++;
+    }
+    double gm;
+    int64_t bad;
+    SWC_TRY(o->eval(o->ctx, SW_EV_UNPLACED, pdst | (nin << 8), c->lanesA, c->lanesB, &gm, &bad));
+    c->steps++;
+    *ok = bad == 0;
+    return 0;
+}
+
 /*
  * The whole sharded plan solve (twin: twin_plan_solve).  Scalar results are
  * global; the engine's SW_EV_FINAL step wrote this rank's plan rows.
@@ -362,7 +414,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         c->steps++;
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
-        int dens_best = 0, dskip_best = 0;
+        int dens_best = 0, dskip_best = 0, rep_best = 0;
         int64_t isum;
         for (int it = 0; it < SW_REPACK_ITERS; ++it) {
             double b0;
@@ -373,7 +425,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             c->steps++;
             int64_t deficit = 0;
             double Jp = 0.0;
-            int dens = 0;
+            int dens = 0, rep = 0;
             for (int ord = -1; ord < 2; ++ord) {
                 const int32_t pdst = ord == 1 ? SW_A_PL2 : SW_A_PL;
                 const int32_t pm = ord < 0 ? 4 : ord ? 3 : 1;
@@ -382,8 +434,18 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                 int64_t dfc;
                 SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, pdst, c->lanesA, c->lanesB, &gm, &dfc));
                 c->steps++;
-                const double Jo = sw_shard_tree(c->lanesA) - c->k * gm;
+                double Jo = sw_shard_tree(c->lanesA) - c->k * gm;
                 if (ord < 0) { /* density order: also the P2 placement when it packs */
+                    int rok = 0;
+                    if (dfc != 0) SWC_RUN(swc_repair(c, SW_A_NB, SW_Y_CUR, SW_A_PL, SW_Y_2, SW_A_PL2, &rok));
+                    if (rok) { /* the repaired placement places every count */
+                        SWC_RUN(o->copy_y(o->ctx, SW_Y_CUR, SW_Y_2));
+                        SWC_RUN(o->copy(o->ctx, SW_A_PL, SW_A_PL2));
+                        SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                        c->steps++;
+                        Jo = sw_shard_tree(c->lanesA) - c->k * gm;
+                        rep = 1;
+                    }
                     if (dfc == 0) { Jp = Jo; dens = 1; break; }
                     continue;
                 }
@@ -400,6 +462,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             if (it == 0 || Jp > Jbest) {
                 Jbest = Jp;
                 dens_best = dens;
+                rep_best = rep;
                 dskip_best = !dens && deficit == 0;
                 SWC_RUN(o->copy(o->ctx, SW_A_NFIN, SW_A_PL));
                 SWC_RUN(o->copy_y(o->ctx, SW_Y_BEST, SW_Y_CUR));
@@ -416,6 +479,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         if (dens_best) { /* (a) is the P1 placement itself */
             SWC_RUN(o->copy_y(o->ctx, SW_Y_2, SW_Y_BEST));
             ok2 = 1;
+            if (rep_best) status |= SW_STATUS_P2_REPAIRED;
         }
         for (int att = 0; att < 2 && !ok2; ++att) {
             if (att == 0 && dskip_best) continue;
@@ -424,16 +488,24 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             SWC_RUN(o->eval(o->ctx, SW_EV_P2OK, 0, c->lanesA, c->lanesB, &gm, &bad));
             c->steps++;
             ok2 = bad == 0;
+            if (!ok2 && att == 0) { /* (a') density with its width profile repaired */
+                SWC_RUN(swc_repair(c, SW_A_NFIN, SW_Y_2, SW_A_PL, SW_Y_CUR, SW_A_PL2, &ok2));
+                if (ok2) {
+                    SWC_RUN(o->copy_y(o->ctx, SW_Y_2, SW_Y_CUR));
+                    status |= SW_STATUS_P2_REPAIRED;
+                }
+            }
             if (ok2 && att == 1) status |= SW_STATUS_P2_WEIGHT_ORDER;
         }
         if (!ok2) {
             int32_t caps[SW_TMAX];
             int32_t wc = 0, next_w = 0;
-            SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, 0, caps, &next_w));
+            int64_t md[2];
+            SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, 0, -1, caps, &next_w, md));
             c->steps++;
             while (next_w != 0x7FFFFFFF) {
                 wc = next_w;
-                SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, wc, caps, &next_w));
+                SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, wc, -1, caps, &next_w, md));
                 c->steps++;
                 SWC_RUN(o->pack_class(o->ctx, SW_A_NFIN, wc, caps, SW_Y_2, SW_A_PL));
                 c->steps++;

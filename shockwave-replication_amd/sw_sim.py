@@ -566,6 +566,7 @@ class Simulator:
             "solves": self.num_solves,
             "solve_seconds": self.solve_seconds,
             "utilization": self.get_cluster_utilization(),
+            "jcts": {str(j): v for j, v in self._job_completion_times.items()},
         }
 
 

@@ -105,7 +105,26 @@ def solve_case(case):
                                             makespan_cap=cap)
     rec["util_at"] = {"status": st, "M_cap": cap, "U": Uu, "M": Mu, "dual_bound": bound,
                       "lp_bound": ub_lp, "seconds": dt + dt_lp}
-    # P2 on the counts the twin (= GPU) plans
+    solve_p2_part(rec)
+    rec["seconds_total"] = time.perf_counter() - t0
+    print(f"{name} seed {seed} G={G}: J_ref {rec['p1']['J']:.9g} J_twin {rec['twin']['J']:.9g} "
+          f"U* {Uu:.6g} U_twin {rec['twin']['U']:.6g} M* {Mmin:.6g} M_twin {rec['twin']['M']:.6g} "
+          f"p2 {rec['twin']['p2_objective'] / max(rec['p2']['objective'], 1e-300):.4f}x  "
+          f"{rec['seconds_total']:.0f}s", flush=True)
+    return rec
+
+
+def solve_p2_part(rec):
+    """The solver-dependent part: the twin's (= the GPU's) planned counts and
+    the reference P2 MILP on exactly those counts (refreshed by --p2-only
+    when the placement algorithm changes; the P1-side oracle stays)."""
+    import milp_ref as mr
+    import ctypes
+    import sw_native as sn
+
+    a = problem((rec["name"], rec["seed"], rec["N"], rec["G"], rec["T"]))
+    assert inputs_digest(a) == rec["inputs_sha"]
+    P = mr.Problem(a.w, a.d, a.F, a.E, a.R, a.p, a.T, a.G, a.delta, a.k, list(a.bases))
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libplan_twin.so"))
     sn.declare_solver_api(lib, "twin_")
     pr, res = a.c_problem(), a.c_result()
@@ -117,11 +136,6 @@ def solve_case(case):
                  "seconds": dt2}
     rec["twin"] = {"J": res.objective, "U": res.utility, "M": res.makespan,
                    "p2_objective": res.p2_objective, "status": res.status}
-    rec["seconds_total"] = time.perf_counter() - t0
-    print(f"{name} seed {seed} G={G}: J_ref {rec['p1']['J']:.9g} J_twin {res.objective:.9g} "
-          f"U* {Uu:.6g} U_twin {res.utility:.6g} M* {Mmin:.6g} M_twin {res.makespan:.6g} "
-          f"p2 {res.p2_objective / max(p2obj, 1e-300):.4f}x  {rec['seconds_total']:.0f}s",
-          flush=True)
     return rec
 
 
@@ -129,7 +143,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=6)
     ap.add_argument("--only", default="")
+    ap.add_argument("--p2-only", dest="p2_only", action="store_true",
+                    help="keep the P1-side oracle records, redo the twin counts and P2 MILPs")
     args = ap.parse_args()
+    if args.p2_only:
+        d = json.load(open(OUT))
+        with mp.get_context("spawn").Pool(args.procs) as pool:
+            d["cases"] = pool.map(solve_p2_part, d["cases"], chunksize=1)
+        for r in d["cases"]:
+            print(r["name"], r["seed"], r["G"], "p2 %.4fx" % (r["twin"]["p2_objective"] /
+                                                           max(r["p2"]["objective"], 1e-300)))
+        json.dump(d, open(OUT, "w"), indent=1)
+        return
     cases = C3_CASES + C5_CASES
     if args.only:
         cases = [c for c in cases if f"{c[0]}:{c[1]}" in args.only.split(",")]

@@ -1,15 +1,15 @@
 """Generates tests/golden/twin_plans.json: plan digests of the CPU twin
-(oracle/plan_twin.c) on seeded instances at the three reference cluster
-configurations (scale_{64,128,256}gpus.json's k and lambda), with the price
-bisection over plain fp32 key bits (the twin as of commit aed1d81).
+(oracle/plan_twin.c) on seeded instances at the reference cluster
+configurations (scale_{32,64,128,256}gpus.json's k and lambda).
 
-The snapped price search must return the same rho* and so
-the same plans; tests/test_twin_plans.py checks the current twin against
-these digests.  Regenerate (only when the algorithm is meant to change):
+History: first pinned with the plain price bisection (commit aed1d81), kept
+through the snapped searches (same results); re-pinned in
+round 2 when the P2 cascade gained the width-profile repair (sw_repair.h),
+which changes placements on purpose.  Performance-only changes must keep
+these digests; tests/test_twin_plans.py checks the twin and the GPU kernel
+against them.  Regenerate only when the algorithm is meant to change:
 
-    git show aed1d81:oracle/plan_twin.c > /tmp/old_twin/plan_twin.c
-    (plus sw_arith.h etc. from the same commit, see build_old below)
-    python tests/golden/make_twin_plans.py /tmp/old_twin/libplan_twin.so
+    python tests/golden/make_twin_plans.py oracle/_build/libplan_twin.so
 """
 import ctypes
 import hashlib
@@ -47,7 +47,7 @@ def digest(lib_path):
 
 if __name__ == "__main__":
     rows = digest(sys.argv[1])
-    json.dump({"source": "oracle/plan_twin.c at aed1d81 (plain price bisection)", "cases": rows},
+    json.dump({"source": "oracle/plan_twin.c, round 2 (P2 width-profile repair)", "cases": rows},
               open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "twin_plans.json"), "w"),
               indent=0)
     print(len(rows), "cases")

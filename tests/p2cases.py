@@ -9,7 +9,7 @@ import sw_native as sn
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "p2_cases.json")
 KIND_BITS = {"density": 0, "weight": sn.SW_STATUS_P2_WEIGHT_ORDER,
-             "classwise": sn.SW_STATUS_P2_CLASSWISE}
+             "classwise": sn.SW_STATUS_P2_CLASSWISE, "repaired": sn.SW_STATUS_P2_REPAIRED}
 
 
 def load_cases():

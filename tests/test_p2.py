@@ -11,14 +11,17 @@ from p2cases import KIND_BITS, arrays, load_cases
 from test_shard import assert_same_as_single, run_threads, shard_lib  # noqa: F401
 
 CASES = load_cases()
-KINDS = ("density", "weight", "classwise")
 # P2 objective of the cascade ÷ HiGHS optimum of the same P2 MILP (gap 1e-4),
-# per placement kind: measured maxima on these cases are ≈1.01 / 1.06 / 1.35
-RATIO_BOUND = {"density": 1.03, "weight": 1.10, "classwise": 1.45}
+# per placement kind actually kept.  The fixture's "kind" labels name what the
+# round-1 cascade kept (density / weight order / class-wise inside the P1
+# profile, up to 1.37x); the density pack with its width-profile repair
+# (sw_repair.h) now places every case the density order strands.  Measured:
+# density <= 1.001, repaired <= 1.034.
+RATIO_BOUND = {"density": 1.01, "repaired": 1.04, "weight": 1.10, "classwise": 1.45}
 
 
 def kind_of(status):
-    for k in ("classwise", "weight"):
+    for k in ("repaired", "classwise", "weight"):
         if status & KIND_BITS[k]:
             return k
     return "density"
@@ -31,7 +34,9 @@ def test_twin_placement_kind_and_validity(twin, i):
     r = twin.solve(a)
     check_plan_valid(a, r)
     assert not (r["status"] & 0x2), "P2 fell back to the P1 placement"
-    assert kind_of(r["status"]) == c["kind"]
+    # cases the density order placed still are; every other one is repaired
+    assert kind_of(r["status"]) in (("density", "repaired") if c["kind"] == "density"
+                                    else ("repaired",))
 
 
 @pytest.mark.parametrize("i", range(len(CASES)))
@@ -45,7 +50,8 @@ def test_twin_p2_objective_vs_milp(twin, i):
     assert y is not None
     ours = mr.p2_objective(prob, r["plan"])
     assert ours >= obj * (1 - 1e-4) - 1e-9  # never better than the optimum (gap)
-    assert ours <= obj * RATIO_BOUND[c["kind"]] + 1e-9, (c["kind"], ours / obj)
+    kind = kind_of(r["status"])
+    assert ours <= obj * RATIO_BOUND[kind] + 1e-9, (kind, ours / obj)
 
 
 @pytest.mark.parametrize("i,tile,world", [(3, 1, 2), (4, 1, 4), (6, 1, 2), (0, 1, 2), (4, 8, 2),

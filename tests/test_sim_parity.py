@@ -3,22 +3,25 @@
 
 Two anchors, both on the reference's 220-job trace with its per-size configs
 (scale_{64,128,256}gpus.json, Δ = 120 s):
-  * the oracle run — the same round loop with every Shockwave plan solved by
+  * the oracle runs — the same round loop with every Shockwave plan solved by
     the MILP restatement of the reference solve (oracle/milp_ref.py, HiGHS,
-    gap 1e-3, 15 s per MILP), tests/golden/sim_milp_220.json;
+    gap 1e-3, 15 s per MILP), tests/golden/sim_milp_220.json.  At 64 GPUs the
+    oracle is run six times on the SAME model with its jobs in different
+    (seeded) orders: HiGHS stops at a different solution inside the gap each
+    time, and the six simulations spread by 3.9 % in makespan, 2.3 % in avg
+    JCT and 3.5 % in worst FTF.  That spread is the reference solver's own
+    indeterminacy (a gap-1e-3 MILP at k = 10 leaves the utility term, which
+    decides who runs among equally ranked jobs, essentially free), so a single
+    oracle run is no sharper a target than the envelope of them;
   * the reference's own published numbers — the bars of
     scheduler/shockwave_replicate/replicated_fig_9.png (read off the PNG,
     ±3 %), tests/golden/fig9_published.json.
 The product solver's schedules come from the CPU twin here (bit-identical to
 the HIP kernels: tests/test_gpu_sim.py).
 
-Tolerances, stated per metric (relative):
-  oracle, 256 / 128 GPUs   makespan, JCT, worst FTF: 1 %
-  oracle, 64 GPUs          makespan, worst FTF: 2 %; avg JCT: 3 % — at 64 GPUs
-                           the plan's last P2 placement decides which of many
-                           equally ranked jobs runs now, and the MILP path itself
-                           moves avg JCT by 0.6 % between gap 1e-3 and 1e-4
-  published bars           5 % (the bars are read to ±3 %)
+Bar: every metric within 1 % of the oracle envelope [min, max] over the
+oracle runs at that size (one run at 128 / 256 GPUs: within 1 % of it);
+published bars 5 % (they are read to ±3 %).
 """
 import contextlib
 import io
@@ -36,7 +39,7 @@ TRACE = os.path.join(st.DATA_DIR, "traces",
                      "220_0.2_5_100_25_4_0,0.5,0.5_0.6,0.3,0.09,0.01_multigpu_dynamic.trace")
 MILP = json.load(open(os.path.join(HERE, "golden", "sim_milp_220.json")))
 FIG9 = json.load(open(os.path.join(HERE, "golden", "fig9_published.json")))
-TOL_ORACLE = {256: (0.01, 0.01, 0.01), 128: (0.01, 0.01, 0.01), 64: (0.02, 0.03, 0.02)}
+TOL = 0.01
 _cache = {}
 
 
@@ -54,20 +57,39 @@ def rel(a, b):
     return abs(a - b) / abs(b)
 
 
+def oracle_runs(gold, prefix):
+    """Every gap-1e-3 oracle run of one configuration (the base run and its
+    job-order permutations)."""
+    runs = [v for k, v in gold.items() if k == prefix or k.startswith(prefix + "_perm")]
+    assert runs, prefix
+    return runs
+
+
+def assert_in_envelope(r, runs, what):
+    assert all(o["jobs_completed"] == r["jobs_completed"] for o in runs), what
+    for key in ("makespan", "avg_jct", "worst_ftf"):
+        lo = min(o[key] for o in runs) * (1 - TOL)
+        hi = max(o[key] for o in runs) * (1 + TOL)
+        assert lo <= r[key] <= hi, (what, key, r[key], lo, hi)
+
+
 @pytest.mark.parametrize("gpus", [256, 128, 64])
 def test_shockwave_metrics_vs_milp_oracle(twin, gpus):
     r = run("shockwave", gpus, twin)
-    o = MILP[f"{gpus}_gap0.001"]
-    assert r["jobs_completed"] == o["jobs_completed"] == 220
-    for key, tol in zip(("makespan", "avg_jct", "worst_ftf"), TOL_ORACLE[gpus]):
-        assert rel(r[key], o[key]) <= tol, (gpus, key, r[key], o[key])
+    assert r["jobs_completed"] == 220
+    assert_in_envelope(r, oracle_runs(MILP, f"{gpus}_gap0.001"), f"{gpus} GPUs")
 
 
 def test_milp_oracle_spread_calibration():
-    """The oracle's own variability (gap 1e-3 vs 1e-4 at 64 GPUs) is the scale
-    the 64-GPU tolerance is set against."""
+    """The oracle's own spread at 64 GPUs: six runs of the same model (job
+    orders permuted) and the gap-1e-4 run.  The spread exceeds the 1 % bar, so
+    the bar is applied to the envelope, not to one run."""
+    runs = oracle_runs(MILP, "64_gap0.001")
+    assert len(runs) == 6
+    for key, least in (("makespan", 0.02), ("avg_jct", 0.01)):
+        vals = [o[key] for o in runs]
+        assert (max(vals) - min(vals)) / min(vals) > least, key
     a, b = MILP["64_gap0.001"], MILP["64_gap0.0001"]
-    assert rel(a["makespan"], b["makespan"]) < 1e-4
     assert rel(a["avg_jct"], b["avg_jct"]) < 0.01
 
 

@@ -2,11 +2,11 @@
 
 tests/golden/twin_plans.json holds, for 32 seeded instances at the reference
 cluster configurations (scale_{32,64,128,256}gpus.json's k and lambda), the
-objective bits and MD5 digests of the plan and counts that the CPU twin
-produced with the price bisection over plain fp32 key bits (commit aed1d81;
-generator: tests/golden/make_twin_plans.py).  The price search is now
-snapped to key values: it must land on the same rho*, so
-the twin and the GPU kernel must both reproduce every digest.
+objective bits and MD5 digests of the plan and counts of the CPU twin
+(generator: tests/golden/make_twin_plans.py; re-pinned when the P2 cascade
+gained the width-profile repair).  Performance-only changes of the kernel or
+the searches must keep them: the twin and the GPU kernel must both reproduce
+every digest.
 """
 import hashlib
 import json
