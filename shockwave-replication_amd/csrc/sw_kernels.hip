@@ -64,6 +64,38 @@ __device__ __forceinline__ uint32_t st_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t st_w(uint32_t s) { return (s >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t st_sel(uint32_t s) { return (s >> 16) & 1u; }
 
+/* Per-job constants of the on-chip path as structure-of-arrays in LDS: a
+ * thread's two jobs sit side by side, so one field of both is one 16-byte LDS
+ * read, and the 34 VGPRs a register copy would pin stay free for the
+ * searches and the packer. */
+struct sw_job_lds {
+    double *rate, *cap, *d, *R, *a, *Fd, *Ed, *invE;
+    int32_t* w;
+    template <class Carve>
+    __device__ __forceinline__ void carve(Carve&& cv) {
+        rate = (double*)cv(8 * SW_LDS_JOBS);
+        cap = (double*)cv(8 * SW_LDS_JOBS);
+        d = (double*)cv(8 * SW_LDS_JOBS);
+        R = (double*)cv(8 * SW_LDS_JOBS);
+        a = (double*)cv(8 * SW_LDS_JOBS);
+        Fd = (double*)cv(8 * SW_LDS_JOBS);
+        Ed = (double*)cv(8 * SW_LDS_JOBS);
+        invE = (double*)cv(8 * SW_LDS_JOBS);
+        w = (int32_t*)cv(4 * SW_LDS_JOBS);
+    }
+    __device__ __forceinline__ sw_jobc get(int j) const {
+        sw_jobc c;
+        c.rate = rate[j]; c.cap = cap[j]; c.d = d[j]; c.R = R[j]; c.a = a[j];
+        c.Fd = Fd[j]; c.Ed = Ed[j]; c.invE = invE[j]; c.w = w[j];
+        return c;
+    }
+    __device__ __forceinline__ void put(int j, const sw_jobc& c) const {
+        rate[j] = c.rate; cap[j] = c.cap; d[j] = c.d; R[j] = c.R; a[j] = c.a;
+        Fd[j] = c.Fd; Ed[j] = c.Ed; invE[j] = c.invE; w[j] = c.w;
+    }
+};
+#define SW_JOB_LDS_BYTES (8 * 8 * SW_LDS_JOBS + 4 * SW_LDS_JOBS)
+
 /* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = SW_JPT · SW_BLOCK) */
 #define SW_JPT 2
 
@@ -101,7 +133,7 @@ struct Ctx {
     int64_t* misc;
     sw_repair_t* rep; /* LDS: the width profile of repair_pack */
     /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
-    sw_jobc jcs[SW_JPT];
+    sw_job_lds JL; /* ONE: per-job constants, SoA in LDS (not VGPRs) */
     float kr[SW_JPT][KT];
     /* per-job data in HBM (!ONE) */
     float* gkeys;
@@ -126,10 +158,10 @@ struct Ctx {
             for (int j = jlo(); j < jhi(); ++j) f(j, 0);
         }
     }
-    __device__ __forceinline__ const sw_jobc& jc(int j, int s) const {
+    __device__ __forceinline__ sw_jobc jc(int j, int s) const {
         if constexpr (ONE) {
-            (void)j;
-            return jcs[s];
+            (void)s;
+            return JL.get(j);
         } else {
             (void)s;
             return gjc[j];
@@ -137,10 +169,12 @@ struct Ctx {
     }
     __device__ __forceinline__ int Tj(int j, int s) const { return jc(j, s).w <= G ? T : 0; }
     __device__ __forceinline__ double fval(int j, int s, int n) const {
-        return sw_f(&jc(j, s), n, nb, beta, ell, slope);
+        const sw_jobc c = jc(j, s);
+        return sw_f(&c, n, nb, beta, ell, slope);
     }
     __device__ __forceinline__ double gval(int j, int s, int n) const {
-        return sw_g(&jc(j, s), n);
+        const sw_jobc c = jc(j, s);
+        return sw_g(&c, n);
     }
 
     __device__ __forceinline__ uint32_t kbits(int j, int s, int n) const {
@@ -263,8 +297,9 @@ struct Ctx {
             for (int s = 0; s < SW_JPT; ++s) {
                 prev[s] = 0.0;
                 vm[s] = 0.0;
-                ksc[s] = sw_key_scale(jcs[s].w, A);
-                if (s < q && jlo() + s < N) prev[s] = sw_f(&jcs[s], 0, nb, beta, ell, slope);
+                const sw_jobc c0 = jc(jlo() + s, s);
+                ksc[s] = sw_key_scale(c0.w, A);
+                if (s < q && jlo() + s < N) prev[s] = sw_f(&c0, 0, nb, beta, ell, slope);
             }
 #pragma unroll
             for (int ch = 0; ch < KT / CH; ++ch) {
@@ -274,8 +309,9 @@ struct Ctx {
                     for (int i = 0; i < CH; ++i) {
                         const int n = ch * CH + i;
                         float kv = 0.0f;
-                        if (act && n < T && jcs[s].w <= G) {
-                            const double cur = sw_f(&jcs[s], n + 1, nb, beta, ell, slope);
+                        const sw_jobc cs = jc(jlo() + s, s);
+                        if (act && n < T && cs.w <= G) {
+                            const double cur = sw_f(&cs, n + 1, nb, beta, ell, slope);
                             const double v = sw_pos(cur - prev[s]);
                             vm[s] = (n == 0) ? v : sw_min(vm[s], v);
                             kv = sw_key(vm[s], ksc[s]);
@@ -1041,7 +1077,7 @@ __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
                r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) + r16(sizeof(sw_repair_t));
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
-        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
+        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK) + SW_JOB_LDS_BYTES;
     }
     return s;
 }
@@ -1117,15 +1153,12 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 4 * SW_JPT * SW_BLOCK);
         c.gkeys = nullptr;
         c.gjc = nullptr;
-#pragma unroll
-        for (int s = 0; s < SW_JPT; ++s) {
-            const int j = c.jlo() + s;
-            if (s < c.q && j < N)
-                c.jcs[s] = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
-                                        B.E[jo + j], B.R[jo + j], B.p[jo + j]);
-            else
-                c.jcs[s] = sw_make_jobc(1, 1, 1.0, 1, 1.0, 0, 1, 0.0, 0.0);
-        }
+        c.JL.carve(carve);
+        /* every slot < SW_LDS_JOBS holds a valid record (a dummy past N) */
+        for (int j = threadIdx.x; j < NJ; j += SW_BLOCK)
+            c.JL.put(j, j < N ? sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
+                                             B.E[jo + j], B.R[jo + j], B.p[jo + j])
+                              : sw_make_jobc(1, 1, 1.0, 1, 1.0, 0, 1, 0.0, 0.0));
     } else {
         uint8_t* u8 = B.ws.u8 + SW_WS_U8 * jo;
         c.ncur = u8 + 0 * (size_t)N;

@@ -19,7 +19,10 @@ import sw_synth as ss  # noqa: E402
 
 
 def main():
-    lib = sn.load(os.path.join(ROOT, "shockwave-replication_amd", "lib", "libshockwave_amd_stamps.so"))
+    path = os.environ.get("SW_STAMPS_LIB") or os.path.join(ROOT, "shockwave-replication_amd", "lib",
+                                                          "libshockwave_amd_stamps.so")
+    print("library:", os.path.relpath(path, ROOT))
+    lib = sn.load(path)
     lib.sw_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     cases = {
         "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] != "-v" else 64)],
