@@ -394,8 +394,14 @@ struct Ctx {
                  * constant between them, and the bracket jumps there.
                  * ca / cb stay exact: no open job has a key strictly
                  * between the snapped end and mid. */
+                int64_t Wb = -1, Wh = -1; /* twin: interpolated probes */
                 while (lo < hi) {
-                    const uint32_t mid = lo + ((hi - lo) >> 1);
+                    uint32_t mid = lo + ((hi - lo) >> 1);
+                    if (Wb >= 0 && Wh >= 0) {
+                        mid = lo + (uint32_t)(((uint64_t)(hi - lo) * (uint64_t)(Wb - bud)) /
+                                              (uint64_t)(Wb - Wh));
+                        if (mid >= hi) mid = hi - 1;
+                    }
                     int32_t wg = 0, mx = 0, mn = 0x7FFFFFFF;
                     for_jobs([&](int j, int s) {
                         int c = cb[s];
@@ -412,12 +418,18 @@ struct Ctx {
                         cb[s] = down ? cm[s] : cb[s];
                         ca[s] = down ? ca[s] : cm[s];
                     }
-                    if (down) hi = (uint32_t)MX > lo ? (uint32_t)MX : lo;
-                    else lo = (uint32_t)MN < hi ? (uint32_t)MN : hi;
+                    if (down) { hi = (uint32_t)MX > lo ? (uint32_t)MX : lo; Wh = wg; }
+                    else { lo = (uint32_t)MN < hi ? (uint32_t)MN : hi; Wb = wg; }
                 }
             } else {
+                int64_t Wb = -1, Wh = -1;
                 while (lo < hi) {
-                    const uint32_t mid = lo + ((hi - lo) >> 1);
+                    uint32_t mid = lo + ((hi - lo) >> 1);
+                    if (Wb >= 0 && Wh >= 0) {
+                        mid = lo + (uint32_t)(((uint64_t)(hi - lo) * (uint64_t)(Wb - bud)) /
+                                              (uint64_t)(Wb - Wh));
+                        if (mid >= hi) mid = hi - 1;
+                    }
                     int32_t wg = 0, mx = 0, mn = 0x7FFFFFFF;
                     for_jobs([&](int j, int s) {
                         const int l = lcur[j];
@@ -429,8 +441,8 @@ struct Ctx {
                     int32_t MX, MN;
                     wg = blk.sum32_max_min(wg, mx, mn, MX, MN);
                     passes++;
-                    if (wg <= bud) hi = (uint32_t)MX > lo ? (uint32_t)MX : lo;
-                    else lo = (uint32_t)MN < hi ? (uint32_t)MN : hi;
+                    if (wg <= bud) { hi = (uint32_t)MX > lo ? (uint32_t)MX : lo; Wh = wg; }
+                    else { lo = (uint32_t)MN < hi ? (uint32_t)MN : hi; Wb = wg; }
                 }
             }
             const uint32_t rho = lo;
@@ -1360,11 +1372,46 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             term = ((double)Ssum / (double)cnt) * c.p_in[j];
         }
         p2 = p2 + term;
-        for (int t = 0; t < T; ++t) plan[(size_t)j * T + t] = (uint8_t)((m >> t) & 1ull);
         B.planned[jo + j] = cnt;
     });
-    const bool any = c.blk.sum(any_l) > 0;
+    const bool any = c.blk.sum(any_l) > 0; /* its barrier: every mask row is final */
     if (!any) status |= SW_STATUS_NO_PLANNED;
+    /* The plan bytes (shockwave.py:390-398 reads x[j][t]): the instance's
+     * N·T-byte range written with aligned 16-byte stores, each thread
+     * expanding 16 consecutive bytes from the round masks (a chunk spans at
+     * most ⌈16/T⌉ + 1 jobs), byte stores only for the unaligned head
+     * and tail — instead of every thread storing its own jobs' bytes one at
+     * a time (strided byte stores that inflated WRITE_SIZE by ~1.6x). */
+    {
+        const uint64_t* ym = ok2 ? c.y2 : c.ybest;
+        const int32_t nbytes = N * T;
+        const int32_t mis = (int32_t)(reinterpret_cast<uintptr_t>(plan) & 15u);
+        const int32_t head = min(nbytes, (16 - mis) & 15);
+        const int32_t nch = (nbytes - head) >> 4;
+        auto byte_at = [&](int32_t b) {
+            const int32_t j = b / T;
+            return (uint8_t)((ym[j] >> (b - j * T)) & 1ull);
+        };
+        for (int32_t b = threadIdx.x; b < head; b += SW_BLOCK) plan[b] = byte_at(b);
+        for (int32_t b = head + nch * 16 + threadIdx.x; b < nbytes; b += SW_BLOCK) plan[b] = byte_at(b);
+        uint4* dst = reinterpret_cast<uint4*>(plan + head);
+        for (int32_t ci = threadIdx.x; ci < nch; ci += SW_BLOCK) {
+            const int32_t b0 = head + ci * 16;
+            int32_t j = b0 / T, t = b0 - j * T;
+            uint64_t m = ym[j];
+            uint32_t wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                wv[k >> 2] |= (uint32_t)((m >> t) & 1ull) << ((k & 3) * 8);
+                if (++t == T) {
+                    t = 0;
+                    ++j;
+                    if (k < 15 && j < N) m = ym[j];
+                }
+            }
+            dst[ci] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
     double U, Mact;
     c.blk.detsum_max(fs, gm, U, Mact);
     const double P2 = c.blk.detsum(p2);
