@@ -471,8 +471,15 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
          * smallest > x, and the bracket jumps to those.  Same answer as a
          * bisection over the fp64 bits of M, in far fewer passes. */
         uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
+        /* probes: the value midpoint until both ends carry a measured F,
+         * then the level where the line through (lo, F just below lo) and
+         * (hi, F(hi)) crosses C (same answer, fewer probes) */
+        int64_t Fb = -1, Fh = -1;
         while (lo < hi) {
             double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+            if (Fb >= 0 && Fh >= 0)
+                x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
+                                           ((double)(Fb - P->C) / (double)(Fb - Fh));
             if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
             if (sw_bits(x) < lo) x = sw_from_bits(lo);
             int64_t F = 0;
@@ -490,8 +497,8 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
                 }
             }
             P->passes++;
-            if (F <= P->C) hi = bmax >= lo ? bmax : lo;
-            else lo = bmin <= hi ? bmin : hi;
+            if (F <= P->C) { hi = bmax >= lo ? bmax : lo; Fh = F; }
+            else { lo = bmin <= hi ? bmin : hi; Fb = F; }
         }
         M_lo = sw_from_bits(lo);
         select_level(P, M_lo, 0, n, l, tk, tmp, &ev, rho_inf, SW_KEY_INF_BITS);

@@ -293,13 +293,34 @@ struct Ctx {
             constexpr int CH = 4;
             float* stage = reinterpret_cast<float*>(sbuf);
             double prev[SW_JPT], vm[SW_JPT], ksc[SW_JPT];
+            /* f(n) = a·φ(u(n)) evaluated incrementally: u(n) is nondecreasing
+             * in n, so the PWL segment sw_phi would select only moves up;
+             * each job keeps its segment's (β_b, ℓ_b, slope_b) and the next
+             * breakpoint in registers and re-reads them from LDS only when u
+             * crosses a breakpoint.  Same operations on the same operands as
+             * sw_f, so the same bits. */
+            int sb[SW_JPT];
+            double sbeta[SW_JPT], sell[SW_JPT], sslope[SW_JPT], snext[SW_JPT];
+            auto seg_load = [&](int s, int b) {
+                sb[s] = b;
+                sbeta[s] = beta[b];
+                sell[s] = ell[b];
+                sslope[s] = slope[b];
+                snext[s] = b + 1 <= nb - 2 ? beta[b + 1] : __builtin_inf();
+            };
+            auto f_inc = [&](int s, const sw_jobc& cj, int n) {
+                const double u = (cj.Fd + sw_e(&cj, n)) * cj.invE;
+                while (snext[s] <= u) seg_load(s, sb[s] + 1);
+                return cj.a * (sell[s] + sslope[s] * (u - sbeta[s]));
+            };
 #pragma unroll
             for (int s = 0; s < SW_JPT; ++s) {
                 prev[s] = 0.0;
                 vm[s] = 0.0;
                 const sw_jobc c0 = jc(jlo() + s, s);
                 ksc[s] = sw_key_scale(c0.w, A);
-                if (s < q && jlo() + s < N) prev[s] = sw_f(&c0, 0, nb, beta, ell, slope);
+                seg_load(s, 0);
+                if (s < q && jlo() + s < N) prev[s] = f_inc(s, c0, 0);
             }
 #pragma unroll
             for (int ch = 0; ch < KT / CH; ++ch) {
@@ -311,7 +332,7 @@ struct Ctx {
                         float kv = 0.0f;
                         const sw_jobc cs = jc(jlo() + s, s);
                         if (act && n < T && cs.w <= G) {
-                            const double cur = sw_f(&cs, n + 1, nb, beta, ell, slope);
+                            const double cur = f_inc(s, cs, n + 1);
                             const double v = sw_pos(cur - prev[s]);
                             vm[s] = (n == 0) ? v : sw_min(vm[s], v);
                             kv = sw_key(vm[s], ksc[s]);
@@ -574,8 +595,12 @@ struct Ctx {
                 lb = blk.dmax(lb);
                 /* twin: the M_lo search that snaps to row values */
                 uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
+                int64_t Fb = -1, Fh = -1; /* twin: interpolated probes */
                 while (lo < hi) {
                     double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+                    if (Fb >= 0 && Fh >= 0)
+                        x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
+                                                   ((double)(Fb - C) / (double)(Fb - Fh));
                     if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
                     if (sw_bits(x) < lo) x = sw_from_bits(lo);
                     int64_t f = 0;
@@ -596,8 +621,8 @@ struct Ctx {
                     uint64_t BMX, BMN;
                     blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
                     passes++;
-                    if (F <= C) hi = BMX >= lo ? BMX : lo;
-                    else lo = BMN <= hi ? BMN : hi;
+                    if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
+                    else { lo = BMN <= hi ? BMN : hi; Fb = F; }
                 }
                 M_lo = sw_from_bits(lo);
                 plo = rho_inf;
