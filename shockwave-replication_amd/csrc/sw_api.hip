@@ -242,9 +242,9 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
     h->total_plan = P;
     h->loaded = true;
 #ifdef SW_STAMPS
-    if (h->d_stamps.reserve((size_t)std::max(count, 1) * 16))
+    if (h->d_stamps.reserve((size_t)std::max(count, 1) * SW_STAMP_SLOTS))
         return fail(h, SW_ERR_HIP, "stamp buffer allocation failed");
-    SW_HIP(h, hipMemset(h->d_stamps.p, 0, (size_t)std::max(count, 1) * 16 * sizeof(uint64_t)));
+    SW_HIP(h, hipMemset(h->d_stamps.p, 0, (size_t)std::max(count, 1) * SW_STAMP_SLOTS * sizeof(uint64_t)));
 #endif
     return SW_OK;
 }
@@ -253,7 +253,7 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
 /* Diagnostic builds only (not part of include/shockwave_amd.h). */
 int sw_debug_stamps(sw_handle* h, uint64_t* out) {
     SW_HIP(h, hipStreamSynchronize(h->stream));
-    SW_HIP(h, hipMemcpy(out, h->d_stamps.p, (size_t)h->count * 16 * sizeof(uint64_t),
+    SW_HIP(h, hipMemcpy(out, h->d_stamps.p, (size_t)h->count * SW_STAMP_SLOTS * sizeof(uint64_t),
                         hipMemcpyDeviceToHost));
     return SW_OK;
 }

@@ -17,6 +17,7 @@
 
 #include "sw_arith.h"
 
+#define SW_STAMP_SLOTS 32 /* per-instance u64 slots of the SW_STAMPS diagnostic build */
 #define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip (2 per thread) */
 
 struct sw_inst_dev {

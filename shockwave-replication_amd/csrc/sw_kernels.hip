@@ -44,13 +44,31 @@ namespace {
         __syncthreads();                                                          \
         if (threadIdx.x == 0 && B.stamps) {                                       \
             uint64_t now_ = __builtin_amdgcn_s_memtime();                         \
-            B.stamps[(size_t)inst_ * 16 + (slot)] += now_ - stamp_prev_;      \
+            B.stamps[(size_t)inst_ * SW_STAMP_SLOTS + (slot)] += now_ - stamp_prev_;      \
             stamp_prev_ = now_;                                                   \
         }                                                                         \
     } while (0)
 #else
 #define SW_STAMP(slot) \
     do {               \
+    } while (0)
+#endif
+
+#ifdef SW_STAMPS
+/* level-search breakdown (thread 0's view), slots 16 + k: 0 force pass,
+ * 1 price probes, 2 tie group, 3 width tail, 4 evaluation, 5 M_lo search,
+ * 6 levels_between */
+#define LS_STAMP(k)                                            \
+    do {                                                       \
+        if (threadIdx.x == 0 && lsp) {                         \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+            lsp[k] += now_ - ls_t;                             \
+            ls_t = now_;                                       \
+        }                                                      \
+    } while (0)
+#else
+#define LS_STAMP(k) \
+    do {            \
     } while (0)
 #endif
 
@@ -116,6 +134,8 @@ struct Ctx {
     const double* p_in;
 #ifdef SW_STAMPS
     uint64_t* swp; /* pack phase stamps of this instance */
+    uint64_t* lsp; /* level-search stamps */
+    uint64_t ls_t;
 #endif
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
     uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
@@ -379,6 +399,7 @@ struct Ctx {
         int64_t Wf, Wall;
         blk.sum2(wf, wall, Wf, Wall);
         passes++;
+        LS_STAMP(0);
         SelEval ev;
         ev.rho = 0;
         if (Wf > C) {
@@ -466,6 +487,7 @@ struct Ctx {
                     else { lo = (uint32_t)MN < hi ? (uint32_t)MN : hi; Wb = wg; }
                 }
             }
+            LS_STAMP(1);
             const uint32_t rho = lo;
             ev.rho = rho;
             rho_d = (double)sw_float_of(rho);
@@ -497,6 +519,7 @@ struct Ctx {
             });
             const int64_t used = blk.sum(used_l);
             passes++;
+            LS_STAMP(2);
             int64_t rem2 = rem - used;
             while (rem2 > 0) {
                 uint64_t best = 0;
@@ -515,6 +538,7 @@ struct Ctx {
                 if (jb >= jlo() && jb < jhi()) ncur[jb] = (uint8_t)(ncur[jb] + 1);
                 rem2 -= w_in[jb];
             }
+            LS_STAMP(3);
         }
         double fs = 0.0, gm = 0.0, ub = 0.0;
         for_jobs([&](int j, int s) {
@@ -526,6 +550,7 @@ struct Ctx {
         ev.J = ev.U - k * ev.Mact;
         ev.ubound = blk.detsum(ub) + (rho_d * A) * (double)(bud - wgt_star);
         passes++;
+        LS_STAMP(4);
         return ev;
     }
 
@@ -556,6 +581,7 @@ struct Ctx {
         });
         c = blk.sum(c);
         passes++;
+        LS_STAMP(6);
         return c;
     }
 
@@ -563,6 +589,9 @@ struct Ctx {
      * Written as a loop over evaluation requests so select_level has a
      * single call site (phase 0: M = +inf; 1: M = M_lo; 2/3: golden m1/m2). */
     __device__ __forceinline__ double level_search() {
+#ifdef SW_STAMPS
+        ls_t = __builtin_amdgcn_s_memtime();
+#endif
         SelEval best, e1, e2;
         best.U = best.Mact = best.ubound = 0.0;
         best.J = -1e308;
@@ -625,6 +654,7 @@ struct Ctx {
                     else { lo = BMN <= hi ? BMN : hi; Fb = F; }
                 }
                 M_lo = sw_from_bits(lo);
+                LS_STAMP(5);
                 plo = rho_inf;
                 phi = SW_KEY_INF_BITS;
                 phase = 1;
@@ -833,7 +863,13 @@ struct Ctx {
                 if (owns(MODE, nin, j)) y[j] = 0;
             });
             const int A_ = (int)blk.sum(act_l);
+#ifdef SW_STAMPS
+            const uint64_t srt0_ = __builtin_amdgcn_s_memtime();
+#endif
             sort_regs(khi, klo);
+#ifdef SW_STAMPS
+            if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
+#endif
             uint32_t st[E];
             uint64_t mk[E];
             int jp[E];
@@ -1141,7 +1177,8 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     const int64_t jo = I->job_off;
     c.w_in = B.w + jo;
 #ifdef SW_STAMPS
-    c.swp = B.stamps ? B.stamps + (size_t)inst_ * 16 + 8 : nullptr;
+    c.swp = B.stamps ? B.stamps + (size_t)inst_ * SW_STAMP_SLOTS + 8 : nullptr;
+    c.lsp = B.stamps ? B.stamps + (size_t)inst_ * SW_STAMP_SLOTS + 16 : nullptr;
 #endif
     c.p_in = B.p + jo;
 
@@ -1453,7 +1490,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         B.out[inst_] = o;
 #ifdef SW_STAMPS
         if (B.stamps) {
-            uint64_t* st = B.stamps + (size_t)inst_ * 16;
+            uint64_t* st = B.stamps + (size_t)inst_ * SW_STAMP_SLOTS;
             st[6] = ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                     (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
             st[7] = rt0_;

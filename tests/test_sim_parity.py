@@ -38,6 +38,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 TRACE = os.path.join(st.DATA_DIR, "traces",
                      "220_0.2_5_100_25_4_0,0.5,0.5_0.6,0.3,0.09,0.01_multigpu_dynamic.trace")
 MILP = json.load(open(os.path.join(HERE, "golden", "sim_milp_220.json")))
+MILP120 = json.load(open(os.path.join(HERE, "golden", "sim_milp_120.json")))
+TRACE120 = os.path.join(st.DATA_DIR, "traces",
+                        "120_0.2_5_100_40_25_0,0.5,0.5_0.6,0.3,0.09,0.01_multigpu_dynamic.trace")
 FIG9 = json.load(open(os.path.join(HERE, "golden", "fig9_published.json")))
 TOL = 0.01
 _cache = {}
@@ -100,3 +103,19 @@ def test_metrics_vs_published_fig9(twin, policy, gpus):
     pub = FIG9[policy][str(gpus)]
     for key in ("makespan", "avg_jct", "worst_ftf"):
         assert rel(r[key], pub[key]) <= 0.05, (policy, gpus, key, r[key], pub[key])
+
+
+@pytest.mark.parametrize("key,gpus,max_jobs", [("C2_64", 64, None), ("C1_32", 32, 50)],
+                         ids=["C2_120jobs_64gpus", "C1_50jobs_32gpus"])
+def test_baseline_c1_c2_vs_milp_oracle(twin, key, gpus, max_jobs):
+    """BASELINE configs 1 and 2: the 120-job trace on 64
+    GPUs, and its first 50 jobs on 32 GPUs (no 50-job trace or 32-GPU JSON
+    exists; scale_64gpus.json is used), against four oracle runs each
+    (tests/golden/sim_milp_120.json)."""
+    cfg = json.load(open(os.path.join(st.DATA_DIR, "configs", "scale_64gpus.json")))
+    with contextlib.redirect_stdout(io.StringIO()):
+        r = sw_sim.run_trace("shockwave", TRACE120, gpus, 120, cfg, shockwave_solver=twin,
+                             mmf_allocator=mmf_ref.twin_allocator, max_jobs=max_jobs)
+    runs = oracle_runs(MILP120, key)
+    assert len(runs) == 4
+    assert_in_envelope(r, runs, key)

@@ -12,6 +12,8 @@ import sys
 
 import numpy as np
 
+SLOTS = 32  # SW_STAMP_SLOTS (csrc/sw_device.h)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shockwave-replication_amd"))
 import sw_native as sn  # noqa: E402
@@ -35,10 +37,12 @@ def main():
         s.upload(batch)
         s.run()
         res = s.download()
-        st = np.zeros(len(batch) * 16, dtype=np.uint64)
+        st = np.zeros(len(batch) * SLOTS, dtype=np.uint64)
         lib.sw_debug_stamps(s.h, st.ctypes.data_as(C.POINTER(C.c_uint64)))
-        st = st.reshape(len(batch), 16).astype(np.float64)
+        st = st.reshape(len(batch), SLOTS).astype(np.float64)
         pk = st[:, 8:14]
+        ls = st[:, 16:23]
+        srt = st[:, 15]
         st = st[:, :6]
         tot = st.sum(axis=1).mean()
         print(f"{name}: mean cycles/instance {tot:.0f}; passes {np.mean([r['iters'] for r in res]):.1f}; "
@@ -48,6 +52,9 @@ def main():
         pnames = ["setup", "hist+need", "tiers", "fill", "tail", "apply"]
         print("   pack round loop (all packs of an instance):",
               " ".join(f"{n} {pk[:, i].mean():.0f}" for i, n in enumerate(pnames)))
+        print(f"   sorts (all packs): {srt.mean():.0f}")
+        lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
+        print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)))
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
             for r, row, prow in list(zip(res, st, pk))[:24]:
                 print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row), "|",
