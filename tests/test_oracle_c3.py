@@ -112,3 +112,26 @@ def test_gpu_vs_oracle_headline_one_launch(gpu_solver):
     rs = gpu_solver.solve_batch(probs)
     for c, a, r in zip(CASES, probs, rs):
         check_against_oracle(c, a, r)
+
+
+@pytest.mark.gpu
+def test_gpu_c5_sweep_512_one_launch(gpu_solver, twin):
+    """BASELINE config 5 at full size: 512 independent 900 x 30 instances
+    (seeds x cluster sizes G in {32, 64, 128, 256}, k / lambda from the
+    matching scale_*gpus.json) in ONE launch of sw_plan_kernel.  The 16
+    oracle-fixture instances ride in the same batch and are held to the oracle
+    bars; all 512 must equal the CPU twin bit for bit and be valid plans."""
+    import sw_synth as ss2
+    from helpers import assert_same_result
+
+    sweep = ss2.sweep_problems(512 - len(CASES), N=900, seed0=700_000)
+    fixed = [problem(c) for c in CASES]
+    batch = fixed + sweep
+    rs = gpu_solver.solve_batch(batch)
+    assert len(rs) == 512
+    for c, a, r in zip(CASES, fixed, rs):
+        check_against_oracle(c, a, r)
+    for i, (a, r) in enumerate(zip(batch, rs)):
+        check_plan_valid(a, r)
+        if i % 4 == 0 or i < len(CASES):  # a quarter of the sweep against the twin (time)
+            assert_same_result(r, twin.solve(a), f"C5 instance {i}")
