@@ -455,88 +455,105 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
     const int32_t N = P->N;
     size_t NN = N > 0 ? (size_t)N : 1;
     sel_eval_t ev, best;
-    select_level(P, 0.0, 1, n, l, tk, tmp, &ev, 0, SW_KEY_INF_BITS);
-    best = ev;
-    const uint32_t rho_inf = ev.rho; /* ρ*(+∞): a lower bound at every level */
-    double U_inf = ev.U, M_free = ev.Mact, ubound_inf = ev.ubound;
+    if (!(N > 0 && P->k > 0.0)) { /* no makespan term: the utility optimum */
+        select_level(P, 0.0, 1, n, l, tk, tmp, &ev, 0, SW_KEY_INF_BITS);
+        memcpy(nb, n, sizeof(int32_t) * NN);
+        return ev.ubound - P->k * ev.Mact;
+    }
+    /* M_lo = the smallest level whose forced rounds fit, min{M : F(M) ≤ C},
+     * F(M) = Σ_j w_j·#{n < T_j : g_j(n) > M}, searched on [lb, top]:
+     * lb = max_j g_j(T_j) (no plan does better), top = max_j g_j(0) (F = 0).
+     * F only steps at the row values g_j(n), so the answer is one of them (or
+     * lb): each probe also returns the largest row value ≤ it and the
+     * smallest > it, and the bracket jumps to those.  Probes: the value
+     * midpoint until both ends carry a measured F, then the level where the
+     * line through (lo, F just below lo) and (hi, F(hi)) crosses C. */
+    double lb = 0.0, top = 0.0;
+    for (int32_t j = 0; j < N; ++j) {
+        lb = sw_max(lb, sw_g(&P->jc[j], P->Tj[j]));
+        top = sw_max(top, sw_g(&P->jc[j], 0));
+    }
+    uint64_t lo = sw_bits(lb), hi = sw_bits(top);
+    int64_t Fb = -1, Fh = -1;
+    while (lo < hi) {
+        double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+        if (Fb >= 0 && Fh >= 0)
+            x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
+                                       ((double)(Fb - P->C) / (double)(Fb - Fh));
+        if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
+        if (sw_bits(x) < lo) x = sw_from_bits(lo);
+        int64_t F = 0;
+        uint64_t bmax = 0, bmin = UINT64_MAX;
+        for (int32_t j = 0; j < N; ++j) {
+            const int32_t c = lforce(P, j, x);
+            F += (int64_t)P->jc[j].w * c;
+            if (c < P->Tj[j]) {
+                const uint64_t b = sw_bits(sw_g(&P->jc[j], c));
+                bmax = b > bmax ? b : bmax;
+            }
+            if (c > 0) {
+                const uint64_t b = sw_bits(sw_g(&P->jc[j], c - 1));
+                bmin = b < bmin ? b : bmin;
+            }
+        }
+        P->passes++;
+        if (F <= P->C) { hi = bmax >= lo ? bmax : lo; Fh = F; }
+        else { lo = bmin <= hi ? bmin : hi; Fb = F; }
+    }
+    const double M_lo = sw_from_bits(lo);
+    sel_eval_t elo;
+    select_level(P, M_lo, 0, n, l, tk, tmp, &elo, 0, SW_KEY_INF_BITS);
+    best = elo;
     memcpy(nb, n, sizeof(int32_t) * NN);
-    double M_lo = M_free;
-    if (N > 0 && P->k > 0.0) {
-        double lb = 0.0;
-        for (int32_t j = 0; j < N; ++j) lb = sw_max(lb, sw_g(&P->jc[j], P->Tj[j]));
-        /* M_lo = the smallest level whose forced rounds fit, min{M : F(M) ≤ C},
-         * F(M) = Σ_j w_j·#{n < T_j : g_j(n) > M}.  F only steps at the row
-         * values g_j(n), so the answer is one of them (or lb): each probe at
-         * the value midpoint x also returns the largest row value ≤ x and the
-         * smallest > x, and the bracket jumps to those.  Same answer as a
-         * bisection over the fp64 bits of M, in far fewer passes. */
-        uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
-        /* probes: the value midpoint until both ends carry a measured F,
-         * then the level where the line through (lo, F just below lo) and
-         * (hi, F(hi)) crosses C (same answer, fewer probes) */
-        int64_t Fb = -1, Fh = -1;
-        while (lo < hi) {
-            double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
-            if (Fb >= 0 && Fh >= 0)
-                x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
-                                           ((double)(Fb - P->C) / (double)(Fb - Fh));
-            if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
-            if (sw_bits(x) < lo) x = sw_from_bits(lo);
-            int64_t F = 0;
-            uint64_t bmax = 0, bmin = UINT64_MAX;
-            for (int32_t j = 0; j < N; ++j) {
-                const int32_t c = lforce(P, j, x);
-                F += (int64_t)P->jc[j].w * c;
-                if (c < P->Tj[j]) {
-                    const uint64_t b = sw_bits(sw_g(&P->jc[j], c));
-                    bmax = b > bmax ? b : bmax;
-                }
-                if (c > 0) {
-                    const uint64_t b = sw_bits(sw_g(&P->jc[j], c - 1));
-                    bmin = b < bmin ? b : bmin;
-                }
-            }
-            P->passes++;
-            if (F <= P->C) { hi = bmax >= lo ? bmax : lo; Fh = F; }
-            else { lo = bmin <= hi ? bmin : hi; Fb = F; }
+    /* Can any higher level win?  A level M > M_lo has J ≤ U_max − k·M with
+     * U_max = Σ_j f_j(T_j), so only levels below M_lo + (U_max − U(M_lo))/k
+     * can; F is constant between row values, so with no row value in that
+     * window M_lo is optimal (ties go to the smaller makespan) and the
+     * utility-only level +∞ is never evaluated — the common case when the
+     * makespan term dominates (k·M ≫ U: the 256- and 64-GPU configurations). */
+    for (int32_t j = 0; j < N; ++j) tmp[j] = fval(P, j, P->Tj[j]);
+    const double U_max = sw_detsum(tmp, N);
+    P->passes++;
+    const double wmax = (U_max - elo.U) / P->k;
+    if (!(wmax > 0.0) || levels_between(P, M_lo, M_lo + wmax) == 0) return elo.ubound - P->k * M_lo;
+    /* the utility-only level +∞: its price is below ρ*(M_lo) */
+    select_level(P, 0.0, 1, n, l, tk, tmp, &ev, 0, elo.rho);
+    if (ev.J > best.J || (ev.J == best.J && ev.Mact < best.Mact)) {
+        best = ev; memcpy(nb, n, sizeof(int32_t) * NN);
+    }
+    const uint32_t rho_inf = ev.rho; /* ρ*(+∞): a lower bound at every level */
+    const double U_inf = ev.U, M_free = ev.Mact, ubound_inf = ev.ubound;
+    /* golden-section search on [a, b] that reuses the surviving interior
+     * point (one new level per shrink); every probe's price is bracketed
+     * by its evaluated neighbours (a and the other interior point, or b) */
+    double width = (U_inf - elo.U) / P->k;
+    double a = M_lo, b = sw_min(M_free, M_lo + width);
+    uint32_t ra = elo.rho, rb = rho_inf; /* ρ*(a); a lower bound of ρ*(b) */
+    if (a < b && levels_between(P, a, b) > 0) {
+        double m1 = a + (b - a) * SW_GS_A;
+        double m2 = a + (b - a) * SW_GS_B;
+        sel_eval_t e1, e2;
+        select_level(P, m1, 0, n, l, tk, tmp, &e1, rb, ra);
+        if (e1.J > best.J || (e1.J == best.J && e1.Mact < best.Mact)) {
+            best = e1; memcpy(nb, n, sizeof(int32_t) * NN);
         }
-        M_lo = sw_from_bits(lo);
-        select_level(P, M_lo, 0, n, l, tk, tmp, &ev, rho_inf, SW_KEY_INF_BITS);
-        if (ev.J > best.J || (ev.J == best.J && ev.Mact < best.Mact)) {
-            best = ev; memcpy(nb, n, sizeof(int32_t) * NN);
+        select_level(P, m2, 0, n, l, tk, tmp, &e2, rb, e1.rho);
+        if (e2.J > best.J || (e2.J == best.J && e2.Mact < best.Mact)) {
+            best = e2; memcpy(nb, n, sizeof(int32_t) * NN);
         }
-        /* golden-section search on [a, b] that reuses the surviving interior
-         * point (one new level per shrink); every probe's price is bracketed
-         * by its evaluated neighbours (a and the other interior point, or b) */
-        double width = (U_inf - ev.U) / P->k;
-        double a = M_lo, b = sw_min(M_free, M_lo + width);
-        uint32_t ra = ev.rho, rb = rho_inf; /* ρ*(a); a lower bound of ρ*(b) */
-        if (a < b && levels_between(P, a, b) > 0) {
-            double m1 = a + (b - a) * SW_GS_A;
-            double m2 = a + (b - a) * SW_GS_B;
-            sel_eval_t e1, e2;
-            select_level(P, m1, 0, n, l, tk, tmp, &e1, rb, ra);
-            if (e1.J > best.J || (e1.J == best.J && e1.Mact < best.Mact)) {
-                best = e1; memcpy(nb, n, sizeof(int32_t) * NN);
-            }
-            select_level(P, m2, 0, n, l, tk, tmp, &e2, rb, e1.rho);
-            if (e2.J > best.J || (e2.J == best.J && e2.Mact < best.Mact)) {
-                best = e2; memcpy(nb, n, sizeof(int32_t) * NN);
-            }
-            for (int it = 0; it < SW_GS_ITERS; ++it) {
-                const int left = e1.J >= e2.J;
-                if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
-                else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
-                if (!(a < b)) break;
-                if (levels_between(P, a, b) == 0) break;
-                sel_eval_t* e = left ? &e1 : &e2;
-                double m;
-                if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
-                else { m2 = a + (b - a) * SW_GS_B; m = m2; }
-                select_level(P, m, 0, n, l, tk, tmp, e, left ? e2.rho : rb, left ? ra : e1.rho);
-                if (e->J > best.J || (e->J == best.J && e->Mact < best.Mact)) {
-                    best = *e; memcpy(nb, n, sizeof(int32_t) * NN);
-                }
+        for (int it = 0; it < SW_GS_ITERS; ++it) {
+            const int left = e1.J >= e2.J;
+            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
+            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
+            if (!(a < b)) break;
+            if (levels_between(P, a, b) == 0) break;
+            sel_eval_t* e = left ? &e1 : &e2;
+            double m;
+            if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
+            else { m2 = a + (b - a) * SW_GS_B; m = m2; }
+            select_level(P, m, 0, n, l, tk, tmp, e, left ? e2.rho : rb, left ? ra : e1.rho);
+            if (e->J > best.J || (e->J == best.J && e->Mact < best.Mact)) {
+                best = *e; memcpy(nb, n, sizeof(int32_t) * NN);
             }
         }
     }

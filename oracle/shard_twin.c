@@ -83,9 +83,9 @@ static int lanes_gather(eng_t* E, const double* v, double* out) {
     return rc;
 }
 
-static int e_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
+static int e_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
     eng_t* E = (eng_t*)ctx;
-    double mx[2] = {0.0, 0.0};
+    double mx[3] = {0.0, 0.0, 0.0};
     for (int32_t i = 0; i < E->NL; ++i) mx[0] = sw_max(mx[0], E->jc[i].a);
     if (E->comm->allreduce_max_f64(E->comm->ctx, mx, 1)) return -1;
     E->A = mx[0];
@@ -100,10 +100,12 @@ static int e_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
             prev = cur;
         }
         mx[1] = sw_max(mx[1], sw_g(&E->jc[i], E->Tj[i]));
+        mx[2] = sw_max(mx[2], sw_g(&E->jc[i], 0));
     }
-    if (E->comm->allreduce_max_f64(E->comm->ctx, mx + 1, 1)) return -1;
+    if (E->comm->allreduce_max_f64(E->comm->ctx, mx + 1, 2)) return -1;
     *A = E->A;
     *lb = mx[1];
+    *top = mx[2];
     /* widths of every job, gathered in padded per-rank blocks */
     int32_t* blk = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1), sizeof(int32_t));
     int32_t* all = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1) * E->world, sizeof(int32_t));
@@ -256,6 +258,8 @@ static int e_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* l
             s += E->arr[SW_A_PL][i] != E->arr[SW_A_NFIN][i];
         } else if (sel == SW_EV_UNPLACED) {
             s += E->arr[arg & 0xFF][i] != E->arr[arg >> 8][i];
+        } else if (sel == SW_EV_UMAX) {
+            va[i] = fv(E, i, E->Tj[i]);
         } else { /* SW_EV_FINAL */
             const uint64_t m = E->y[arg][i];
             int32_t cn = 0;

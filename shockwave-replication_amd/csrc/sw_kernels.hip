@@ -587,86 +587,106 @@ struct Ctx {
 
     /* twin: level_search — best counts land in nbest; returns the bound.
      * Written as a loop over evaluation requests so select_level has a
-     * single call site (phase 0: M = +inf; 1: M = M_lo; 2/3: golden m1/m2). */
+     * single call site (phase 1: M = M_lo; 0: M = +inf; 2 / 3: the first
+     * golden pair m1, m2; 4 / 5: the new m1 / m2 after a shrink that kept
+     * the other point). */
     __device__ __forceinline__ double level_search() {
 #ifdef SW_STAMPS
         ls_t = __builtin_amdgcn_s_memtime();
 #endif
-        SelEval best, e1, e2;
+        SelEval best, e1, e2, elo;
         best.U = best.Mact = best.ubound = 0.0;
         best.J = -1e308;
         best.rho = 0;
         e1 = best;
         e2 = best;
-        double U_inf = 0.0, M_free = 0.0, ub_inf = 0.0, M_lo = 0.0;
+        elo = best;
+        double M_lo = 0.0, ret = 0.0;
         double a = 0.0, b = 0.0, m1 = 0.0, m2 = 0.0;
-        uint32_t rho_inf = 0, ra = 0, rb = 0, plo = 0, phi = SW_KEY_INF_BITS;
-        /* phase 0: M = +inf; 1: M_lo; 2 / 3: the first golden pair m1, m2;
-         * 4 / 5: the new m1 / m2 after a shrink that kept the other point */
-        int phase = 0, it = 0;
+        uint32_t rb = 0, ra = 0, plo = 0, phi = SW_KEY_INF_BITS;
+        const bool levels = N > 0 && k > 0.0;
+        if (levels) {
+            /* twin: the M_lo search on [lb, top] that snaps to row values */
+            double lb = 0.0, top = 0.0;
+            for_jobs([&](int j, int s) {
+                lb = sw_max(lb, gval(j, s, Tj(j, s)));
+                top = sw_max(top, gval(j, s, 0));
+            });
+            lb = blk.dmax(lb);
+            top = blk.dmax(top);
+            uint64_t lo = sw_bits(lb), hi = sw_bits(top);
+            int64_t Fb = -1, Fh = -1; /* twin: interpolated probes */
+            while (lo < hi) {
+                double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
+                if (Fb >= 0 && Fh >= 0)
+                    x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
+                                               ((double)(Fb - C) / (double)(Fb - Fh));
+                if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
+                if (sw_bits(x) < lo) x = sw_from_bits(lo);
+                int64_t f = 0;
+                uint64_t bmx = 0, bmn = ~0ull;
+                for_jobs([&](int j, int s) {
+                    const int cn = lforce(j, s, x);
+                    f += (int64_t)jc(j, s).w * cn;
+                    if (cn < Tj(j, s)) {
+                        const uint64_t bb = sw_bits(gval(j, s, cn));
+                        bmx = bb > bmx ? bb : bmx;
+                    }
+                    if (cn > 0) {
+                        const uint64_t bb = sw_bits(gval(j, s, cn - 1));
+                        bmn = bb < bmn ? bb : bmn;
+                    }
+                });
+                int64_t F;
+                uint64_t BMX, BMN;
+                blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
+                passes++;
+                if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
+                else { lo = BMN <= hi ? BMN : hi; Fb = F; }
+            }
+            M_lo = sw_from_bits(lo);
+            LS_STAMP(5);
+        }
+        int phase = levels ? 1 : 0, it = 0;
         while (true) {
             double M = 0.0;
             if (phase == 1) M = M_lo;
             else if (phase == 2 || phase == 4) M = m1;
             else if (phase >= 3) M = m2;
             const SelEval ev = select_level(M, phase == 0, plo, phi);
-            if (phase == 0) {
+            if (phase == 1) {
                 best = ev;
+                elo = ev;
                 for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
-                U_inf = ev.U;
-                M_free = ev.Mact;
-                ub_inf = ev.ubound;
-                M_lo = M_free;
-                rho_inf = ev.rho;
-                if (!(N > 0 && k > 0.0)) break;
-                double lb = 0.0;
-                for_jobs([&](int j, int s) { lb = sw_max(lb, gval(j, s, Tj(j, s))); });
-                lb = blk.dmax(lb);
-                /* twin: the M_lo search that snaps to row values */
-                uint64_t lo = sw_bits(lb), hi = sw_bits(M_free);
-                int64_t Fb = -1, Fh = -1; /* twin: interpolated probes */
-                while (lo < hi) {
-                    double x = (sw_from_bits(lo) + sw_from_bits(hi)) * 0.5;
-                    if (Fb >= 0 && Fh >= 0)
-                        x = sw_from_bits(lo) + (sw_from_bits(hi) - sw_from_bits(lo)) *
-                                                   ((double)(Fb - C) / (double)(Fb - Fh));
-                    if (sw_bits(x) >= hi) x = sw_from_bits(hi - 1);
-                    if (sw_bits(x) < lo) x = sw_from_bits(lo);
-                    int64_t f = 0;
-                    uint64_t bmx = 0, bmn = ~0ull;
-                    for_jobs([&](int j, int s) {
-                        const int cn = lforce(j, s, x);
-                        f += (int64_t)jc(j, s).w * cn;
-                        if (cn < Tj(j, s)) {
-                            const uint64_t b = sw_bits(gval(j, s, cn));
-                            bmx = b > bmx ? b : bmx;
-                        }
-                        if (cn > 0) {
-                            const uint64_t b = sw_bits(gval(j, s, cn - 1));
-                            bmn = b < bmn ? b : bmn;
-                        }
-                    });
-                    int64_t F;
-                    uint64_t BMX, BMN;
-                    blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
-                    passes++;
-                    if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
-                    else { lo = BMN <= hi ? BMN : hi; Fb = F; }
-                }
-                M_lo = sw_from_bits(lo);
-                LS_STAMP(5);
-                plo = rho_inf;
-                phi = SW_KEY_INF_BITS;
-                phase = 1;
+                /* twin: can a higher level win?  Only below
+                 * M_lo + (U_max − U(M_lo))/k, U_max = Σ_j f_j(T_j) */
+                double um = 0.0;
+                for_jobs([&](int j, int s) { um = um + fval(j, s, Tj(j, s)); });
+                const double U_max = blk.detsum(um);
+                passes++;
+                const double wmax = (U_max - ev.U) / k;
+                ret = ev.ubound - k * M_lo;
+                if (!(wmax > 0.0)) break;
+                if (levels_between(M_lo, M_lo + wmax) == 0) break;
+                plo = 0;
+                phi = ev.rho; /* ρ*(+∞) ≤ ρ*(M_lo) */
+                phase = 0;
                 continue;
             }
-            keep_best(ev, best);
-            if (phase == 1) {
-                const double width = (U_inf - ev.U) / k;
+            if (phase == 0) {
+                if (!levels) { /* no makespan term: the utility optimum */
+                    best = ev;
+                    for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
+                    ret = ev.ubound - k * ev.Mact;
+                    break;
+                }
+                keep_best(ev, best);
+                ret = ev.ubound - k * M_lo;
+                const double width = (ev.U - elo.U) / k;
                 a = M_lo;
-                b = sw_min(M_free, M_lo + width);
-                ra = ev.rho;
-                rb = rho_inf;
+                b = sw_min(ev.Mact, M_lo + width);
+                ra = elo.rho;
+                rb = ev.rho;
                 it = 0;
                 if (!(a < b)) break;
                 if (levels_between(a, b) == 0) break;
@@ -677,6 +697,7 @@ struct Ctx {
                 phase = 2;
                 continue;
             }
+            keep_best(ev, best);
             if (phase == 2) {
                 e1 = ev;
                 plo = rb;
@@ -706,7 +727,7 @@ struct Ctx {
             }
         }
         __syncthreads();
-        return ub_inf - k * M_lo;
+        return ret;
     }
 
     /* ---- packing ---------------------------------------------------------- */

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
                                                const double* d, const int32_t* F,
                                                const int32_t* E, const double* R, double delta) {
     const int i = blockIdx.x * kTB + threadIdx.x;
-    uint64_t amax = 0, lb = 0, bad = 0;
+    uint64_t amax = 0, lb = 0, top = 0, bad = 0;
     if (i < S.NL) {
         /* the per-job checks of sw_validate_problem, on the device: device-
          * resident inputs (sw_dist_plan_solve_dev) never visit the host */
@@ -156,11 +156,13 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
             jc[i] = c;
             amax = sw_bits(c.a); /* a, g ≥ 0: bit order = value order */
             lb = sw_bits(sw_g(&c, tj_of(S, c)));
+            top = sw_bits(sw_g(&c, 0));
         }
     }
     red_umax(S.red + 0, amax);
     red_umax(S.red + 1, lb);
     red_umax(S.red + 2, bad);
+    red_umax(S.red + 3, top);
 }
 
 /* key rows (twin: build), A read from the all-reduced step result */
@@ -442,6 +444,8 @@ __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const in
             is = S.arr[SW_A_PL][i] != S.arr[SW_A_NFIN][i];
         } else if (sel == SW_EV_UNPLACED) {
             is = S.arr[arr_a][i] != S.arr[arr_b][i];
+        } else if (sel == SW_EV_UMAX) {
+            fa = sw_f(&c, tj_of(S, c), S.nb, S.beta, S.ell, S.slope);
         } else { /* SW_EV_FINAL */
             const uint64_t m = ysrc[i];
             const int cn = __popcll(m);
@@ -844,14 +848,14 @@ int zero_red(sw_shard_state* S, int n) {
 
 /* ---- sw_shard_ops ---------------------------------------------------------- */
 
-int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
+int op_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
-    SH_TRY(zero_red(S, 3));
+    SH_TRY(zero_red(S, 4));
     LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->in_w, S->in_d, S->in_F,
            S->in_E, S->in_R, S->delta);
-    uint64_t mx[3];
-    SH_TRY(coll_reduce(S, S->dv.red, 3, 1, mx));
+    uint64_t mx[4];
+    SH_TRY(coll_reduce(S, S->dv.red, 4, 1, mx));
     if (mx[2]) return S->h->err = "invalid problem (per-job inputs)", SW_ERR_INVALID; /* every rank */
     if (S->host_comm && S->world > 1) { /* kernels read A from red[0] */
         memcpy(S->hx.p, mx, 16);
@@ -861,6 +865,7 @@ int op_setup(void* ctx, double* A, double* lb, int32_t* w_all) {
     LAUNCH(S, k_keys, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv);
     *A = sw_from_bits(mx[0]);
     *lb = sw_from_bits(mx[1]);
+    *top = sw_from_bits(mx[3]);
     /* every job's width, gathered once (the width tail needs w of the winner) */
     int32_t* wsend = (int32_t*)S->xsend.p;
     int32_t* wrecv = (int32_t*)S->xrecv.p;

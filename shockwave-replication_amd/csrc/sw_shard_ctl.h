@@ -66,14 +66,15 @@ enum {
     SW_EV_P2OK = 3,   /* isum: #{j : placed ≠ nfin}                                  */
     SW_EV_FINAL = 4,  /* y = Y[arg]: c = popcount(y); A: f(c)  B: S(y)/c·p  gm: g(c)
                          isum: #{c > 0}; also writes the plan rows and counts        */
-    SW_EV_UNPLACED = 5 /* isum: #{j : arr[arg & 0xFF]_j ≠ arr[arg >> 8]_j}           */
+    SW_EV_UNPLACED = 5, /* isum: #{j : arr[arg & 0xFF]_j ≠ arr[arg >> 8]_j}          */
+    SW_EV_UMAX = 6      /* A: f(T_j) (every job all its rounds)                       */
 };
 
 typedef struct sw_shard_ops {
     void* ctx;
-    /* constants, key rows; A = max_j a_j, lb = max_j g_j(T_j); w_all[N] = every
-     * job's width (gathered) */
-    int (*setup)(void* ctx, double* A, double* lb, int32_t* w_all);
+    /* constants, key rows; A = max_j a_j, lb = max_j g_j(T_j), top = max_j
+     * g_j(0); w_all[N] = every job's width (gathered) */
+    int (*setup)(void* ctx, double* A, double* lb, double* top, int32_t* w_all);
     /* l_j := #{n < T_j : g_j(n) > M} (0 if is_inf); out = (Σ w·l, Σ w·(T_j − l)) */
     int (*force)(void* ctx, double M, int32_t is_inf, int64_t out[2]);
     /* out[i] = Σ w·#{n ∈ [l_j, T_j) : key_j(n) > rho[i]} */
@@ -158,7 +159,7 @@ typedef struct {
     int64_t N;
     int32_t T, G;
     int64_t C;
-    double k, A, lb;
+    double k, A, lb, top;
     int32_t* w_all;
     int64_t steps; /* collective steps taken (reported as iters) */
     double lanesA[SW_DET_LANES], lanesB[SW_DET_LANES];
@@ -282,54 +283,72 @@ static inline int swc_keep(sw_shard_ctl* c, const sw_shard_eval* e, sw_shard_eva
     return 0;
 }
 
-/* twin: level_search — best counts in SW_A_NB; *bound = U∞bound − k·M_lo */
+/* twin: level_search — best counts in SW_A_NB; *bound as the twin */
 static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
     const sw_shard_ops* o = c->ops;
-    sw_shard_eval ev, best;
-    SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, SW_KEY_INF_BITS));
-    best = ev;
+    sw_shard_eval ev, best, elo;
+    if (!(c->N > 0 && c->k > 0.0)) { /* no makespan term: the utility optimum */
+        SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, SW_KEY_INF_BITS));
+        SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
+        *bound = ev.ubound - c->k * ev.Mact;
+        return 0;
+    }
+    uint64_t lo;
+    SWC_TRY(swc_search(c, 1, sw_bits(c->lb), sw_bits(c->top), c->C, &lo));
+    const double M_lo = sw_from_bits(lo);
+    SWC_TRY(swc_select(c, M_lo, 0, &elo, 0, SW_KEY_INF_BITS));
+    best = elo;
+    SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
+    /* a higher level can win only below M_lo + (U_max − U(M_lo))/k (twin) */
+    double gm;
+    int64_t isum, nbw = 0;
+    SWC_TRY(o->eval(o->ctx, SW_EV_UMAX, 0, c->lanesA, c->lanesB, &gm, &isum));
+    c->steps++;
+    const double U_max = sw_shard_tree(c->lanesA);
+    const double wmax = (U_max - elo.U) / c->k;
+    if (wmax > 0.0) {
+        SWC_TRY(o->between(o->ctx, M_lo, M_lo + wmax, &nbw));
+        c->steps++;
+    }
+    if (nbw == 0) {
+        *bound = elo.ubound - c->k * M_lo;
+        return 0;
+    }
+    SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, elo.rho));
+    SWC_TRY(swc_keep(c, &ev, &best));
     const uint32_t rho_inf = ev.rho;
     const double U_inf = ev.U, M_free = ev.Mact, ub_inf = ev.ubound;
-    SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
-    double M_lo = M_free;
-    if (c->N > 0 && c->k > 0.0) {
-        uint64_t lo;
-        SWC_TRY(swc_search(c, 1, sw_bits(c->lb), sw_bits(M_free), c->C, &lo));
-        M_lo = sw_from_bits(lo);
-        SWC_TRY(swc_select(c, M_lo, 0, &ev, rho_inf, SW_KEY_INF_BITS));
-        SWC_TRY(swc_keep(c, &ev, &best));
-        /* golden section with the surviving interior point reused (twin) */
-        const double width = (U_inf - ev.U) / c->k;
-        double a = M_lo, b = sw_min(M_free, M_lo + width);
-        uint32_t ra = ev.rho, rb = rho_inf;
-        int64_t nbw = 0;
-        if (a < b) {
+    /* golden section with the surviving interior point reused (twin) */
+    const double width = (U_inf - elo.U) / c->k;
+    double a = M_lo, b = sw_min(M_free, M_lo + width);
+    uint32_t ra = elo.rho, rb = rho_inf;
+    nbw = 0;
+    if (a < b) {
+        SWC_TRY(o->between(o->ctx, a, b, &nbw));
+        c->steps++;
+    }
+    if (a < b && nbw > 0) {
+        double m1 = a + (b - a) * SW_GS_A;
+        double m2 = a + (b - a) * SW_GS_B;
+        sw_shard_eval e1, e2;
+        SWC_TRY(swc_select(c, m1, 0, &e1, rb, ra));
+        SWC_TRY(swc_keep(c, &e1, &best));
+        SWC_TRY(swc_select(c, m2, 0, &e2, rb, e1.rho));
+        SWC_TRY(swc_keep(c, &e2, &best));
+        for (int it = 0; it < SW_GS_ITERS; ++it) {
+            const int left = e1.J >= e2.J;
+            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
+            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
+            if (!(a < b)) break;
             SWC_TRY(o->between(o->ctx, a, b, &nbw));
             c->steps++;
-        }
-        if (a < b && nbw > 0) {
-            double m1 = a + (b - a) * SW_GS_A;
-            double m2 = a + (b - a) * SW_GS_B;
-            sw_shard_eval e1, e2;
-            SWC_TRY(swc_select(c, m1, 0, &e1, rb, ra));
-            SWC_TRY(swc_keep(c, &e1, &best));
-            SWC_TRY(swc_select(c, m2, 0, &e2, rb, e1.rho));
-            SWC_TRY(swc_keep(c, &e2, &best));
-            for (int it = 0; it < SW_GS_ITERS; ++it) {
-                const int left = e1.J >= e2.J;
-                if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
-                else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
-                if (!(a < b)) break;
-                SWC_TRY(o->between(o->ctx, a, b, &nbw));
-                c->steps++;
-                if (nbw == 0) break;
-                sw_shard_eval* e = left ? &e1 : &e2;
-                double m;
-                if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
-                else { m2 = a + (b - a) * SW_GS_B; m = m2; }
-                SWC_TRY(swc_select(c, m, 0, e, left ? e2.rho : rb, left ? ra : e1.rho));
-                SWC_TRY(swc_keep(c, e, &best));
-            }
+            if (nbw == 0) break;
+            sw_shard_eval* e = left ? &e1 : &e2;
+            double m;
+            if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
+            else { m2 = a + (b - a) * SW_GS_B; m = m2; }
+            SWC_TRY(swc_select(c, m, 0, e, left ? e2.rho : rb, left ? ra : e1.rho));
+            SWC_TRY(swc_keep(c, e, &best));
         }
     }
     *bound = ub_inf - c->k * M_lo;
@@ -410,7 +429,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         if (rc < 0) goto done;       \
     } while (0)
     {
-        SWC_RUN(o->setup(o->ctx, &c->A, &c->lb, c->w_all));
+        SWC_RUN(o->setup(o->ctx, &c->A, &c->lb, &c->top, c->w_all));
         c->steps++;
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
