@@ -123,6 +123,7 @@ struct Ctx {
     int32_t N, T, G, nb, q;
     int64_t C;
     double k, A;
+    double inv_delta; /* 1 / Δ: the slope of g(n) ≈ R − Δ·n (d·rate = Δ) */
     int64_t passes;
     const sw_inst_dev* inst;
     const double* beta; /* LDS */
@@ -230,7 +231,48 @@ struct Ctx {
     }
     /* twin: lforce */
     __device__ __forceinline__ int lforce(int j, int s, double M) const {
-        return g_count_gt(jc(j, s), Tj(j, s), M);
+        double gi, gb;
+        return lforce_g(j, s, M, gi, gb);
+    }
+    /* The same count with the row values either side of it: gi = g(cnt)
+     * (when cnt < Tj) and gb = g(cnt − 1) (when cnt > 0).  g is
+     * nonincreasing, flat from where e(n) reaches its cap and otherwise
+     * g(n) = R − d·rate·n = R − Δ·n up to rounding, so the count is guessed
+     * from (R − M)/Δ and settled by an exact walk on sw_g — two or three
+     * evaluations instead of a 5-step binary search plus two. */
+    __device__ __forceinline__ int lforce_g(int j, int s, double M, double& gi, double& gb) const {
+        const sw_jobc c = jc(j, s);
+        const int tj = Tj(j, s);
+        if (tj == 0) return 0;
+        const double gl = sw_g(&c, tj - 1);
+        if (gl > M) { /* every round is forced (the flat tail is above M) */
+            gb = gl;
+            return tj;
+        }
+        /* the answer is the smallest n < tj with g(n) ≤ M */
+        const double x = (c.R - M) * inv_delta;
+        int n = x <= 0.0 ? 0 : (x >= (double)(tj - 1) ? tj - 1 : (int)ceil(x));
+        double gn = n == tj - 1 ? gl : sw_g(&c, n);
+        if (gn > M) {
+            do {
+                gb = gn;
+                ++n;
+                gn = n == tj - 1 ? gl : sw_g(&c, n);
+            } while (gn > M);
+            gi = gn;
+            return n;
+        }
+        gi = gn;
+        while (n > 0) {
+            const double gp = sw_g(&c, n - 1);
+            if (gp > M) {
+                gb = gp;
+                break;
+            }
+            gi = gp;
+            --n;
+        }
+        return n;
     }
     /* twin: cnt_gt / cnt_ge.  Keys are nonincreasing, so the items with
      * key > ρ (≥ ρ) form a prefix [0, c) and the count over [l, Tj) is
@@ -626,14 +668,15 @@ struct Ctx {
                 int64_t f = 0;
                 uint64_t bmx = 0, bmn = ~0ull;
                 for_jobs([&](int j, int s) {
-                    const int cn = lforce(j, s, x);
+                    double gi = 0.0, gb = 0.0;
+                    const int cn = lforce_g(j, s, x, gi, gb);
                     f += (int64_t)jc(j, s).w * cn;
                     if (cn < Tj(j, s)) {
-                        const uint64_t bb = sw_bits(gval(j, s, cn));
+                        const uint64_t bb = sw_bits(gi);
                         bmx = bb > bmx ? bb : bmx;
                     }
                     if (cn > 0) {
-                        const uint64_t bb = sw_bits(gval(j, s, cn - 1));
+                        const uint64_t bb = sw_bits(gb);
                         bmn = bb < bmn ? bb : bmn;
                     }
                 });
@@ -1192,6 +1235,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.nb = I->nb;
     c.C = (int64_t)I->G * I->T;
     c.k = I->k;
+    c.inv_delta = 1.0 / I->delta;
     c.passes = 0;
     c.q = (c.N + SW_BLOCK - 1) / SW_BLOCK;
     const int N = c.N;
