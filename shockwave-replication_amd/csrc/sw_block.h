@@ -80,6 +80,58 @@ __device__ __forceinline__ int32_t wave_sufscan_i32(int32_t v) {
     return __builtin_amdgcn_readlane(inc, 63) - inc + v;
 }
 
+/* 64-bit wave reductions on DPP: each step moves both halves with the same
+ * row_shr / row_bcast pattern as the integer scans (two DPP movs) and keeps
+ * the larger / smaller; lanes without a source read the identity.  Used for
+ * every max / min the block reductions take (the shuffle versions below cost
+ * two ds_bpermute round trips per step). */
+#define SW_DPP64(x, idv, ctrl, rm)                                                              \
+    ((((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)((idv) >> 32),            \
+                                                       (int)(uint32_t)((x) >> 32), ctrl, rm,    \
+                                                       0xF, false)) << 32) |                    \
+     (uint64_t)(uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(idv), (int)(uint32_t)(x),  \
+                                                     ctrl, rm, 0xF, false))
+#define SW_DPP64_STEPS(STEP) STEP(0x111, 0xF) STEP(0x112, 0xF) STEP(0x114, 0xF) STEP(0x118, 0xF) \
+    STEP(0x142, 0xA) STEP(0x143, 0xC)
+
+__device__ __forceinline__ uint64_t sw_readlane63_u64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#define SW_MAXU_(c, rm)                               \
+    {                                                 \
+        const uint64_t y_ = SW_DPP64(x, 0ull, c, rm); \
+        x = y_ > x ? y_ : x;                          \
+    }
+    SW_DPP64_STEPS(SW_MAXU_)
+#undef SW_MAXU_
+    return sw_readlane63_u64(x);
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#define SW_MINU_(c, rm)                                \
+    {                                                  \
+        const uint64_t y_ = SW_DPP64(x, ~0ull, c, rm); \
+        x = y_ < x ? y_ : x;                           \
+    }
+    SW_DPP64_STEPS(SW_MINU_)
+#undef SW_MINU_
+    return sw_readlane63_u64(x);
+}
+/* max of doubles (identity −inf) */
+__device__ __forceinline__ double wave_max_f64(double v) {
+    uint64_t x = __builtin_bit_cast(uint64_t, v);
+#define SW_MAXD_(c, rm)                                                       \
+    {                                                                         \
+        const uint64_t y_ = SW_DPP64(x, 0xFFF0000000000000ull, c, rm);        \
+        x = __builtin_bit_cast(double, y_) > __builtin_bit_cast(double, x) ? y_ : x; \
+    }
+    SW_DPP64_STEPS(SW_MAXD_)
+#undef SW_MAXD_
+    return __builtin_bit_cast(double, sw_readlane63_u64(x));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -213,7 +265,7 @@ struct sw_blk {
     }
 
     __device__ __forceinline__ uint64_t umax(uint64_t v) {
-        v = wave_max(v);
+        v = wave_max_u64(v);
         if (lane_id() == 0) X->u[par][wave_id()] = v;
         __syncthreads();
         uint64_t m = 0;
@@ -224,7 +276,7 @@ struct sw_blk {
     }
 
     __device__ __forceinline__ double dmax(double v) {
-        v = wave_max(v);
+        v = wave_max_f64(v);
         if (lane_id() == 0) X->d[par][wave_id()][0] = v;
         __syncthreads();
         double m = X->d[par][0][0];
@@ -238,8 +290,8 @@ struct sw_blk {
     __device__ __forceinline__ void sum_max_min(int64_t v, uint64_t mx, uint64_t mn, int64_t& S,
                                                 uint64_t& MX, uint64_t& MN) {
         const int64_t w = wave_sum_i32((int32_t)v);
-        mx = wave_max(mx);
-        mn = wave_min(mn);
+        mx = wave_max_u64(mx);
+        mn = wave_min_u64(mn);
         if (lane_id() == 0) {
             X->i[par][wave_id()][0] = w;
             X->u2[par][wave_id()][0] = mx;
@@ -291,7 +343,7 @@ struct sw_blk {
     /* sw_detsum of the per-thread partials v, and the max of m, together. */
     __device__ __forceinline__ void detsum_max(double v, double m, double& S, double& M) {
         v = wave_dettree(v);
-        m = wave_max(m);
+        m = wave_max_f64(m);
         if (lane_id() == 0) { X->d[par][wave_id()][0] = v; X->d[par][wave_id()][1] = m; }
         __syncthreads();
         double s[SW_WAVES];

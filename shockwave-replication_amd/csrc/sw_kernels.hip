@@ -1494,8 +1494,13 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         gm = sw_max(gm, c.gval(j, s, cnt));
         double term = 0.0;
         if (cnt > 0) {
-            int64_t Ssum = 0;
-            for (int t = 0; t < T; ++t) Ssum += ((m >> t) & 1ull) ? t : 0;
+            /* Σ_t t·bit_t of the mask: bit b of t weighted 2^b, six popcounts */
+            const int64_t Ssum = (int64_t)__popcll(m & 0xAAAAAAAAAAAAAAAAull) +
+                                 2 * (int64_t)__popcll(m & 0xCCCCCCCCCCCCCCCCull) +
+                                 4 * (int64_t)__popcll(m & 0xF0F0F0F0F0F0F0F0ull) +
+                                 8 * (int64_t)__popcll(m & 0xFF00FF00FF00FF00ull) +
+                                 16 * (int64_t)__popcll(m & 0xFFFF0000FFFF0000ull) +
+                                 32 * (int64_t)__popcll(m & 0xFFFFFFFF00000000ull);
             term = ((double)Ssum / (double)cnt) * c.p_in[j];
         }
         p2 = p2 + term;
