@@ -380,7 +380,7 @@ static int repair_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin
         for (int32_t j = 0; j < N; ++j) {
             const int cls = nin[j] > 0 && P->jc[j].w == R.wc[c];
             nc[j] = cls ? nin[j] : 0;
-            k1[j] = cls ? sw_bits(pr->priority[j] / (double)nin[j]) : 0;
+            k1[j] = cls ? sw_ratio_key(pr->priority[j] / (double)nin[j]) : 0;
         }
         pack(P, nc, k1, k2, yc, pc, R.caps[c], 1);
         for (int32_t j = 0; j < N; ++j)
@@ -605,7 +605,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         for (int ord = -1; ord < 2; ++ord) {
             for (int32_t j = 0; j < N; ++j) {
                 if (ord < 0) {
-                    k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] / (double)(nb[j] * P.jc[j].w)) : 0;
+                    k1[j] = nb[j] > 0 ? sw_ratio_key(pr->priority[j] / (double)(nb[j] * P.jc[j].w)) : 0;
                     k2[j] = 0;
                 } else if (nb[j] > 0) {
                     double lvl = sw_g(&P.jc[j], nb[j] - 1);
@@ -690,7 +690,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     for (int att = 0; att < 2 && !ok2; ++att) {
         if (att == 0 && dskip_best) continue;
         for (int32_t j = 0; j < N; ++j) {
-            k1[j] = nb[j] > 0 ? sw_bits(pr->priority[j] /
+            k1[j] = nb[j] > 0 ? sw_ratio_key(pr->priority[j] /
                                         (double)(att == 0 ? nb[j] * P.jc[j].w : nb[j]))
                               : 0;
             k2[j] = 0;
@@ -725,7 +725,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
             for (int32_t j = 0; j < N; ++j) {
                 int cls = nb[j] > 0 && P.jc[j].w == wc;
                 nc[j] = cls ? nb[j] : 0;
-                k1[j] = cls ? sw_bits(pr->priority[j] / (double)nb[j]) : 0;
+                k1[j] = cls ? sw_ratio_key(pr->priority[j] / (double)nb[j]) : 0;
                 k2[j] = 0;
                 if (cls)
                     for (int32_t t = 0; t < T; ++t) caps[t] += y1[(size_t)j * T + t];

@@ -324,7 +324,7 @@ static int e_pack_any(eng_t* E, int32_t mode, int32_t src, double Mb, int32_t yd
         mine[i].nin = n;
         if (n > 0) {
             if (mode == 4) {
-                mine[i].k1 = sw_bits(E->p[i] / (double)(n * E->jc[i].w));
+                mine[i].k1 = sw_ratio_key(E->p[i] / (double)(n * E->jc[i].w));
                 mine[i].k2 = 0;
             } else if (mode != 2 && mode != 5) {
                 const double lvl = sw_g(&E->jc[i], n - 1);
@@ -332,7 +332,7 @@ static int e_pack_any(eng_t* E, int32_t mode, int32_t src, double Mb, int32_t yd
                 mine[i].k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)E->jc[i].w : 0);
                 mine[i].k2 = sw_fbits_of(KEY(E, i, n - 1));
             } else {
-                mine[i].k1 = sw_bits(E->p[i] / (double)n);
+                mine[i].k1 = sw_ratio_key(E->p[i] / (double)n);
                 mine[i].k2 = 0;
             }
         }

@@ -138,6 +138,13 @@ SW_HD float sw_key(double vm, double scale) {
 
 SW_HD double sw_pos(double v) { return v > 0.0 ? v : 0.0; }
 
+/* Placement-order key of a priority ratio (p_j/(n_j·w_j) or p_j/n_j, ≥ 0):
+ * the fp64 bits without the 11 lowest mantissa bits (relative resolution
+ * 2^-41), so that on the on-chip path the key and an 11-bit job index share
+ * one 64-bit word and the placement sort moves 64 bits per element, not 128.
+ * Ratios that agree to 2^-41 are ordered by job index, like exact ties. */
+SW_HD uint64_t sw_ratio_key(double r) { return sw_bits(r) >> 11; }
+
 /* Golden-section constants (fp64 literals, identical on both sides). */
 #define SW_GS_A 0.3819660112501051
 #define SW_GS_B 0.6180339887498949

@@ -840,6 +840,59 @@ struct Ctx {
         }
     }
 
+    /* sort_regs for one 64-bit key per element (the ratio orders of pack
+     * modes 2 / 4 / 5: sw_ratio_key << 11 | (2047 − job)): the same network,
+     * half the data through the shuffles and the LDS exchange. */
+    __device__ __forceinline__ void sort_regs64(uint64_t (&k)[SW_JPT]) {
+        constexpr int E = SW_JPT;
+        constexpr int NE = E * SW_BLOCK;
+        const int tid = threadIdx.x;
+        int buf = 0;
+        for (int kk = 2; kk <= NE; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                if (jj < E) {
+#pragma unroll
+                    for (int s = 0; s < E; ++s) {
+                        if ((s & jj) == 0) {
+                            const int t2 = s | jj;
+                            const bool up = ((E * tid + s) & kk) == 0;
+                            const bool gt = k[s] > k[t2];
+                            if (up ? !gt : gt) {
+                                const uint64_t tk = k[s];
+                                k[s] = k[t2];
+                                k[t2] = tk;
+                            }
+                        }
+                    }
+                    continue;
+                }
+                uint64_t pk[E];
+                const int tj = jj / E;
+                if (tj >= 64) {
+                    uint64_t* xk = sbuf + (size_t)buf * NE;
+#pragma unroll
+                    for (int s = 0; s < E; ++s) xk[E * tid + s] = k[s];
+                    __syncthreads();
+#pragma unroll
+                    for (int s = 0; s < E; ++s) pk[s] = xk[(E * tid + s) ^ jj];
+                    buf ^= 1;
+                } else {
+#pragma unroll
+                    for (int s = 0; s < E; ++s) pk[s] = __shfl_xor(k[s], tj, 64);
+                }
+#pragma unroll
+                for (int s = 0; s < E; ++s) {
+                    const int e = E * tid + s;
+                    const bool up = (e & kk) == 0;
+                    const bool lower = (e & jj) == 0;
+                    const bool mine_gt = k[s] > pk[s];
+                    const bool keep_max = (lower == up);
+                    if (keep_max ? !mine_gt : mine_gt) k[s] = pk[s];
+                }
+            }
+        }
+    }
+
     /* Sort in the HBM workspace (!ONE): bitonic over NP entries. */
     __device__ __forceinline__ void sort_global(int NP) {
         uint64_t* shi = sbuf;
@@ -882,7 +935,7 @@ struct Ctx {
             uint64_t k1;
             uint32_t k2;
             if (MODE == 4) {
-                k1 = sw_bits(p_in[j] / (double)(nj * jc(j, s).w));
+                k1 = sw_ratio_key(p_in[j] / (double)(nj * jc(j, s).w));
                 k2 = 0;
             } else if (MODE != 2 && MODE != 5) {
                 const double lvl = gval(j, s, nj - 1);
@@ -890,7 +943,7 @@ struct Ctx {
                 k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (MODE == 3 ? (uint64_t)jc(j, s).w : 0);
                 k2 = kbits(j, s, nj - 1);
             } else {
-                k1 = sw_bits(p_in[j] / (double)nj);
+                k1 = sw_ratio_key(p_in[j] / (double)nj);
                 k2 = 0;
             }
             khi = k1;
@@ -930,7 +983,21 @@ struct Ctx {
 #ifdef SW_STAMPS
             const uint64_t srt0_ = __builtin_amdgcn_s_memtime();
 #endif
-            sort_regs(khi, klo);
+            /* the ratio orders (modes 2, 4, 5: k2 = 0) sort one 64-bit word
+             * per job, key << 11 | (2047 − job) (N ≤ SW_LDS_JOBS), exactly
+             * the order (k1 desc, job asc); the P1 orders 1 / 3 sort (k1, k2,
+             * job) as two words */
+            const bool ratio = MODE == 2 || MODE == 4 || MODE == 5;
+            if (ratio) {
+#pragma unroll
+                for (int s = 0; s < E; ++s)
+                    khi[s] = khi[s] != 0 || klo[s] != 0
+                                 ? (khi[s] << 11) | (uint64_t)(2047u - (0xFFFFFFFFu - (uint32_t)klo[s]))
+                                 : 0ull;
+                sort_regs64(khi);
+            } else {
+                sort_regs(khi, klo);
+            }
 #ifdef SW_STAMPS
             if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
 #endif
@@ -941,7 +1008,8 @@ struct Ctx {
             for (int s = 0; s < E; ++s) {
                 const int p = E * (int)threadIdx.x + s;
                 mk[s] = 0;
-                jp[s] = (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
+                jp[s] = ratio ? (int)(2047u - (uint32_t)(khi[s] & 2047u))
+                              : (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
                 const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
                 st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
             }

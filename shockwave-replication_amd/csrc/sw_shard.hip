@@ -512,7 +512,7 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
             uint64_t k1;
             uint32_t k2;
             if (mode == 4) {
-                k1 = sw_bits(S.p[i] / (double)(n * c.w));
+                k1 = sw_ratio_key(S.p[i] / (double)(n * c.w));
                 k2 = 0;
             } else if (mode != 2 && mode != 5) {
                 const double lvl = sw_g(&c, n - 1);
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
                 k1 = crit ? (SW_CRIT_BIT | sw_bits(lvl)) : (mode == 3 ? (uint64_t)c.w : 0);
                 k2 = sw_fbits_of(S.keys[(size_t)i * S.T + n - 1]);
             } else {
-                k1 = sw_bits(S.p[i] / (double)n);
+                k1 = sw_ratio_key(S.p[i] / (double)n);
                 k2 = 0;
             }
             e.khi = k1;
