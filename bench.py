@@ -112,6 +112,9 @@ def parse():
                     help="sharded C4 solves timed for the c4_sharded sub-record")
     ap.add_argument("--no-c4", dest="no_c4", action="store_true",
                     help="skip the sharded C4 sub-record of the default line")
+    ap.add_argument("--no-legs", dest="no_legs", action="store_true",
+                    help="profiling runs: skip the host-boundary / single-instance / sustained "
+                         "legs and the C4 sub-record")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -281,7 +284,7 @@ def main():
     traffic = pmc_traffic(args.batch, args.jobs, args.rounds)
 
     extra = {}
-    if rank == 0:
+    if rank == 0 and not args.no_legs:
         extra = boundary_legs(args, solver, batch, results, local)
     solver.close()
     cpu = None
@@ -292,7 +295,7 @@ def main():
             cpu = {"value": None, "unit": "plan-solves/s", "cores": 1, "kind": "port",
                    "sample": f"failed: {e!r}"}
     c4 = None
-    if not args.no_c4:
+    if not (args.no_c4 or args.no_legs):
         c4 = c4_leg(args, world, rank, local, dist)
     if rank == 0:
         cyc = avg_kernel_s * CLOCK_HZ * min(NUM_CU, args.batch) / args.batch

@@ -9,7 +9,7 @@ B=${2:-2048}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --batch $B"
+CMD="python3 bench.py --no-cpu-baseline --no-legs --steps 3 --warmup 1 --batch $B"
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- $CMD > $OUT/stats.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $CMD > $OUT/fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $CMD > $OUT/write.log 2>&1 &&
