@@ -109,6 +109,9 @@ __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int 
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
         int32_t cap = caps ? caps[t] : G;
+#ifdef SW_STAMPS
+        if (threadIdx.x == 0 && swp) swp[17] += 1; /* rounds */
+#endif
         __syncthreads(); /* Hu holds the placements of round t − 1 */
         /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
          * lane m holds hv = H[m + 1] */
@@ -128,6 +131,9 @@ __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int 
             const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
             if (mask == 0) break;
             const int m = 63 - __builtin_clzll(mask);
+#ifdef SW_STAMPS
+            if (threadIdx.x == 0 && swp) swp[18] += 1; /* active tiers */
+#endif
             const int32_t q = __shfl(need, m, 64) - red;
             int32_t lt = 0;
 #pragma unroll
@@ -186,6 +192,9 @@ __device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int 
                 best = ok ? (((E * tid + i) << 8) | (int32_t)pk_w(st[i])) : best;
             }
             best = blk.min32(best);
+#ifdef SW_STAMPS
+            if (threadIdx.x == 0 && swp) swp[19] += 1; /* width-tail reductions */
+#endif
             if (best == 0x7FFFFFFF) break;
             const int pos = best >> 8;
 #pragma unroll

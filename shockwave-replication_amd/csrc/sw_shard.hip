@@ -57,7 +57,7 @@
 
 #ifdef SW_STAMPS
 /* diagnostic builds: k_pack_rounds phase cycles (sw_pack.h SWP_STAMP) */
-__device__ uint64_t g_sw_pack_stamps[8];
+__device__ uint64_t g_sw_pack_stamps[24]; /* swp[0..7] phases, [17..19] counters */
 #endif
 
 namespace {
@@ -1075,6 +1075,12 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
                capsd);
     else if (M <= 8 * SW_BLOCK)
         LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
+    else if (M <= 16 * SW_BLOCK)
+        LAUNCH(S, k_pack_rounds<16>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
+               capsd);
+    else if (M <= 20 * SW_BLOCK) /* the 10k-job C4 shape: every position slot is a job */
+        LAUNCH(S, k_pack_rounds<20>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
                capsd);
     else if (M <= 32 * SW_BLOCK)
         LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,

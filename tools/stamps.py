@@ -43,6 +43,7 @@ def main():
         pk = st[:, 8:14]
         ls = st[:, 16:23]
         srt = st[:, 15]
+        scans, misses, rounds = st[:, 26].mean(), st[:, 27].mean(), st[:, 25].mean()
         st = st[:, :6]
         tot = st.sum(axis=1).mean()
         print(f"{name}: mean cycles/instance {tot:.0f}; passes {np.mean([r['iters'] for r in res]):.1f}; "
@@ -52,7 +53,8 @@ def main():
         pnames = ["setup", "hist+need", "tiers", "fill", "tail", "apply"]
         print("   pack round loop (all packs of an instance):",
               " ".join(f"{n} {pk[:, i].mean():.0f}" for i, n in enumerate(pnames)))
-        print(f"   sorts (all packs): {srt.mean():.0f}")
+        print(f"   sorts (all packs): {srt.mean():.0f}; rounds {rounds:.1f}, active tiers {scans:.1f}, "
+              f"width-tail reductions {misses:.1f}")
         lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
         print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)))
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
