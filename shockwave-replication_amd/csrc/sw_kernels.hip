@@ -1013,26 +1013,61 @@ struct Ctx {
                 const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
                 st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
             }
-            #ifdef SW_STAMPS
-            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp,
-                                   swp);
-#else
-            sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp);
-#endif
-            for_jobs([&](int j, int s) {
-                (void)s;
-                if (owns(MODE, nin, j)) placed_out[j] = 0;
-            });
-            __syncthreads();
+            if (A_ <= SW_BLOCK) {
+                /* at most one position per thread (a C3 instance places
+                 * ~1/3 of its jobs): redistribute through LDS so that thread
+                 * t owns position t, and every pass of the round loop walks
+                 * one position instead of E (the sort's LDS exchange buffer
+                 * is free once every wave has left the sort) */
+                uint64_t* xp = sbuf;
+                __syncthreads();
 #pragma unroll
-            for (int s = 0; s < E; ++s) {
-                const int p = E * (int)threadIdx.x + s;
-                if (p < A_) {
-                    y[jp[s]] = mk[s];
-                    placed_out[jp[s]] = (uint8_t)(nin[jp[s]] - st_r(st[s]));
+                for (int s = 0; s < E; ++s) {
+                    const int p = E * (int)threadIdx.x + s;
+                    if (p < A_) xp[p] = ((uint64_t)(uint32_t)jp[s] << 32) | st[s];
                 }
+                __syncthreads();
+                const bool mine = (int)threadIdx.x < A_;
+                const uint64_t e = mine ? xp[threadIdx.x] : 0ull;
+                uint32_t st1[1] = {(uint32_t)e};
+                uint64_t mk1[1] = {0ull};
+                const int jp1 = (int)(e >> 32);
+#ifdef SW_STAMPS
+                sw_pack_rounds<1>(blk, PL, A_, T, G, st1, mk1, capsp, swp);
+#else
+                sw_pack_rounds<1>(blk, PL, A_, T, G, st1, mk1, capsp);
+#endif
+                for_jobs([&](int j, int s) {
+                    (void)s;
+                    if (owns(MODE, nin, j)) placed_out[j] = 0;
+                });
+                __syncthreads();
+                if (mine) {
+                    y[jp1] = mk1[0];
+                    placed_out[jp1] = (uint8_t)(nin[jp1] - st_r(st1[0]));
+                }
+                __syncthreads();
+            } else {
+#ifdef SW_STAMPS
+                sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp, swp);
+#else
+                sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp);
+#endif
+                for_jobs([&](int j, int s) {
+                    (void)s;
+                    if (owns(MODE, nin, j)) placed_out[j] = 0;
+                });
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < E; ++s) {
+                    const int p = E * (int)threadIdx.x + s;
+                    if (p < A_) {
+                        y[jp[s]] = mk[s];
+                        placed_out[jp[s]] = (uint8_t)(nin[jp[s]] - st_r(st[s]));
+                    }
+                }
+                __syncthreads();
             }
-            __syncthreads();
         } else {
             int NPg = 1;
             while (NPg < N) NPg <<= 1;

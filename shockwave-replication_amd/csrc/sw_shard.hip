@@ -642,23 +642,11 @@ __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, cons
 /* capsd: per-round capacities of the class-wise repack (nullptr = G); then
  * only the entries' rows are written, every other job is left untouched */
 template <int E>
-__global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
-                                                          int64_t M, const int32_t* order,
-                                                          uint64_t* ydst, int32_t* pdst,
-                                                          const int32_t* capsd) {
-    __shared__ sw_xchg X;
-    __shared__ sw_pack_lds PL;
-    __shared__ int32_t capsL[64];
-    sw_blk blk;
-    blk.X = &X;
-    blk.par = 0;
+__device__ __forceinline__ void pack_rounds_body(const ShardDev& S, const sw_pack_ent* all, int A,
+                                                 const int32_t* order, uint64_t* ydst, int32_t* pdst,
+                                                 const int32_t* capsd, sw_blk& blk, sw_pack_lds* PL,
+                                                 const int32_t* capsL) {
     const int tid = threadIdx.x;
-    if (capsd && tid < S.T) capsL[tid] = capsd[tid];
-    int act = 0;
-    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
-    const int A = blk.sum32(act); /* its barrier publishes capsL */
-    if (!capsd)
-        for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
     uint32_t st[E];
     uint64_t mk[E];
     int32_t ent[E];
@@ -671,10 +659,10 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
         st[i] = E * tid + i < A ? v : 0u;
         ent[i] = E * tid + i < A ? ent[i] : -1;
     }
-    #ifdef SW_STAMPS
-    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr, g_sw_pack_stamps);
+#ifdef SW_STAMPS
+    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr, g_sw_pack_stamps);
 #else
-    sw_pack_rounds<E>(blk, &PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr);
+    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr);
 #endif
 #pragma unroll
     for (int i = 0; i < E; ++i) {
@@ -685,6 +673,35 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
             pdst[j - S.off] = (int32_t)(all[ent[i]].st & 0xFFu) - (int32_t)pk_r(st[i]);
         }
     }
+}
+
+/* The round loop with E positions per thread.  The launch sizes E from the
+ * entries M, but only the ACTIVE entries (jobs with rounds to place — about
+ * 3/8 of a C4 instance's jobs) take positions, and every pass of the loop
+ * walks all E.  So the host launches the variant for M and, when M is large,
+ * a smaller one too; each counts the active entries A and runs only when
+ * alo < A ≤ E·SW_BLOCK (one runs, the other returns at once).  Separate
+ * kernels keep each variant's registers to its own E. */
+template <int E>
+__global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
+                                                          int64_t M, const int32_t* order,
+                                                          uint64_t* ydst, int32_t* pdst,
+                                                          const int32_t* capsd, int alo) {
+    __shared__ sw_xchg X;
+    __shared__ sw_pack_lds PL;
+    __shared__ int32_t capsL[64];
+    sw_blk blk;
+    blk.X = &X;
+    blk.par = 0;
+    const int tid = threadIdx.x;
+    if (capsd && tid < S.T) capsL[tid] = capsd[tid];
+    int act = 0;
+    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
+    const int A = blk.sum32(act); /* its barrier publishes capsL */
+    if (A <= alo || A > E * SW_BLOCK) return; /* the other variant places these */
+    if (!capsd)
+        for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
+    pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
 }
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n + kTB - 1) / kTB : 1); }
@@ -1070,26 +1087,28 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     const ShardDev dv = S->dv;
     uint64_t* yd = S->y[ydst].p;
     int32_t* pd = S->arr[pdst].p;
-    if (M <= 2 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<2>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else if (M <= 8 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<8>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else if (M <= 16 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<16>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else if (M <= 20 * SW_BLOCK) /* the 10k-job C4 shape: every position slot is a job */
-        LAUNCH(S, k_pack_rounds<20>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else if (M <= 32 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<32>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else if (M <= 64 * SW_BLOCK)
-        LAUNCH(S, k_pack_rounds<64>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, pd,
-               capsd);
-    else
+    /* variants by entries M; above 8 positions per thread also the 8-position
+     * variant, for instances whose active jobs fit it (k_pack_rounds) */
+#define SW_LAUNCH_PACK(E, ALO)                                                                \
+    LAUNCH(S, k_pack_rounds<E>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, \
+           pd, capsd, (int)(ALO))
+    if (M <= 2 * SW_BLOCK) {
+        SW_LAUNCH_PACK(2, -1);
+    } else if (M <= 8 * SW_BLOCK) {
+        SW_LAUNCH_PACK(8, -1);
+    } else if (M <= 20 * SW_BLOCK) {
+        SW_LAUNCH_PACK(8, -1);
+        SW_LAUNCH_PACK(20, 8 * SW_BLOCK);
+    } else if (M <= 32 * SW_BLOCK) {
+        SW_LAUNCH_PACK(8, -1);
+        SW_LAUNCH_PACK(32, 8 * SW_BLOCK);
+    } else if (M <= 64 * SW_BLOCK) {
+        SW_LAUNCH_PACK(8, -1);
+        SW_LAUNCH_PACK(64, 8 * SW_BLOCK);
+    } else {
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
+    }
+#undef SW_LAUNCH_PACK
     if (mode == 5) SH_HIP(S, hipStreamSynchronize(st)); /* hcaps is reused by the next class */
     return SW_OK;
 }
