@@ -283,14 +283,17 @@ static inline int swc_keep(sw_shard_ctl* c, const sw_shard_eval* e, sw_shard_eva
     return 0;
 }
 
-/* twin: level_search — best counts in SW_A_NB; *bound as the twin */
-static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
+/* twin: level_search — best counts in SW_A_NB; *bound as the twin; *mk =
+ * the makespan max_j g_j(nb_j) of those counts, which the winning level's
+ * SELECT evaluation already reduced (so the solve needs no GMAX step) */
+static inline int swc_level_search(sw_shard_ctl* c, double* bound, double* mk) {
     const sw_shard_ops* o = c->ops;
     sw_shard_eval ev, best, elo;
     if (!(c->N > 0 && c->k > 0.0)) { /* no makespan term: the utility optimum */
         SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, SW_KEY_INF_BITS));
         SWC_TRY(o->copy(o->ctx, SW_A_NB, SW_A_N));
         *bound = ev.ubound - c->k * ev.Mact;
+        *mk = ev.Mact;
         return 0;
     }
     uint64_t lo;
@@ -312,6 +315,7 @@ static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
     }
     if (nbw == 0) {
         *bound = elo.ubound - c->k * M_lo;
+        *mk = best.Mact;
         return 0;
     }
     SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, elo.rho));
@@ -352,6 +356,7 @@ static inline int swc_level_search(sw_shard_ctl* c, double* bound) {
         }
     }
     *bound = ub_inf - c->k * M_lo;
+    *mk = best.Mact;
     return 0;
 }
 
@@ -434,14 +439,10 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
         int dens_best = 0, dskip_best = 0, rep_best = 0;
-        int64_t isum;
         for (int it = 0; it < SW_REPACK_ITERS; ++it) {
-            double b0;
-            SWC_RUN(swc_level_search(c, &b0));
+            double b0, Mb;
+            SWC_RUN(swc_level_search(c, &b0, &Mb));
             if (it == 0) bound = b0;
-            double Mb;
-            SWC_RUN(o->eval(o->ctx, SW_EV_GMAX, SW_A_NB, c->lanesA, c->lanesB, &Mb, &isum));
-            c->steps++;
             int64_t deficit = 0;
             double Jp = 0.0;
             int dens = 0, rep = 0;
