@@ -893,6 +893,41 @@ struct Ctx {
         }
     }
 
+    /* Descending bitonic sort of SW_BLOCK keys, one per thread (the compacted
+     * active jobs of a pack, pack()): strides < 64 pair lanes of one wave
+     * (shuffles), larger ones go through a double-buffered LDS exchange at
+     * x (4·SW_BLOCK words).  TWO: (hi, lo) pairs; else hi alone. */
+    template <bool TWO>
+    __device__ __forceinline__ void sort_one(uint64_t& hi, uint64_t& lo, uint64_t* x) {
+        const int e = (int)threadIdx.x;
+        int buf = 0;
+        for (int kk = 2; kk <= SW_BLOCK; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                uint64_t ph, pl = 0;
+                if (jj >= 64) {
+                    uint64_t* xh = x + (size_t)buf * 2 * SW_BLOCK;
+                    uint64_t* xl = xh + SW_BLOCK;
+                    xh[e] = hi;
+                    if (TWO) xl[e] = lo;
+                    __syncthreads();
+                    ph = xh[e ^ jj];
+                    if (TWO) pl = xl[e ^ jj];
+                    buf ^= 1;
+                } else {
+                    ph = __shfl_xor(hi, jj, 64);
+                    if (TWO) pl = __shfl_xor(lo, jj, 64);
+                }
+                const bool up = (e & kk) == 0;
+                const bool lower = (e & jj) == 0;
+                const bool mine_gt = TWO ? (hi > ph) || (hi == ph && lo > pl) : hi > ph;
+                if ((lower == up) ? !mine_gt : mine_gt) {
+                    hi = ph;
+                    if (TWO) lo = pl;
+                }
+            }
+        }
+    }
+
     /* Sort in the HBM workspace (!ONE): bitonic over NP entries. */
     __device__ __forceinline__ void sort_global(int NP) {
         uint64_t* shi = sbuf;
@@ -979,7 +1014,11 @@ struct Ctx {
                 act_l += nin_of(MODE, nin, j) > 0;
                 if (owns(MODE, nin, j)) y[j] = 0;
             });
-            const int A_ = (int)blk.sum(act_l);
+            /* the active jobs' slots in job order (klo ≠ 0 exactly when the
+             * job brings rounds); the total is A */
+            int32_t A32;
+            const int32_t abase = blk.exscan((int32_t)act_l, A32);
+            const int A_ = A32;
 #ifdef SW_STAMPS
             const uint64_t srt0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -994,44 +1033,38 @@ struct Ctx {
                     khi[s] = khi[s] != 0 || klo[s] != 0
                                  ? (khi[s] << 11) | (uint64_t)(2047u - (0xFFFFFFFFu - (uint32_t)klo[s]))
                                  : 0ull;
-                sort_regs64(khi);
-            } else {
-                sort_regs(khi, klo);
-            }
-#ifdef SW_STAMPS
-            if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
-#endif
-            uint32_t st[E];
-            uint64_t mk[E];
-            int jp[E];
-#pragma unroll
-            for (int s = 0; s < E; ++s) {
-                const int p = E * (int)threadIdx.x + s;
-                mk[s] = 0;
-                jp[s] = ratio ? (int)(2047u - (uint32_t)(khi[s] & 2047u))
-                              : (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
-                const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
-                st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
             }
             if (A_ <= SW_BLOCK) {
-                /* at most one position per thread (a C3 instance places
-                 * ~1/3 of its jobs): redistribute through LDS so that thread
-                 * t owns position t, and every pass of the round loop walks
-                 * one position instead of E (the sort's LDS exchange buffer
-                 * is free once every wave has left the sort) */
-                uint64_t* xp = sbuf;
-                __syncthreads();
+                /* at most one position per thread (a C3 instance places ~1/3
+                 * of its jobs): compact the active keys through LDS, sort
+                 * SW_BLOCK of them one per thread (half the network of the
+                 * 1024-slot sort), and thread t owns position t, so every pass
+                 * of the round loop walks one position instead of E */
+                uint64_t* xh = sbuf;
+                uint64_t* xl = sbuf + SW_BLOCK;
+                int b = abase;
 #pragma unroll
-                for (int s = 0; s < E; ++s) {
-                    const int p = E * (int)threadIdx.x + s;
-                    if (p < A_) xp[p] = ((uint64_t)(uint32_t)jp[s] << 32) | st[s];
-                }
+                for (int s = 0; s < E; ++s)
+                    if (klo[s] != 0) {
+                        xh[b] = khi[s];
+                        xl[b] = klo[s];
+                        ++b;
+                    }
                 __syncthreads();
                 const bool mine = (int)threadIdx.x < A_;
-                const uint64_t e = mine ? xp[threadIdx.x] : 0ull;
-                uint32_t st1[1] = {(uint32_t)e};
+                uint64_t h1 = mine ? xh[threadIdx.x] : 0ull;
+                uint64_t l1 = mine ? xl[threadIdx.x] : 0ull;
+                if (ratio) sort_one<false>(h1, l1, sbuf + 2 * SW_BLOCK);
+                else sort_one<true>(h1, l1, sbuf + 2 * SW_BLOCK);
+#ifdef SW_STAMPS
+                if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
+#endif
+                const int jp1 = !mine ? 0
+                                : ratio ? (int)(2047u - (uint32_t)(h1 & 2047u))
+                                        : (int)(0xFFFFFFFFu - (uint32_t)(l1 & 0xFFFFFFFFu));
+                const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp1];
+                uint32_t st1[1] = {mine ? ((uint32_t)nin[jp1] | (wq << 8)) : 0u};
                 uint64_t mk1[1] = {0ull};
-                const int jp1 = (int)(e >> 32);
 #ifdef SW_STAMPS
                 sw_pack_rounds<1>(blk, PL, A_, T, G, st1, mk1, capsp, swp);
 #else
@@ -1048,6 +1081,23 @@ struct Ctx {
                 }
                 __syncthreads();
             } else {
+                if (ratio) sort_regs64(khi);
+                else sort_regs(khi, klo);
+#ifdef SW_STAMPS
+                if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
+#endif
+                uint32_t st[E];
+                uint64_t mk[E];
+                int jp[E];
+#pragma unroll
+                for (int s = 0; s < E; ++s) {
+                    const int p = E * (int)threadIdx.x + s;
+                    mk[s] = 0;
+                    jp[s] = ratio ? (int)(2047u - (uint32_t)(khi[s] & 2047u))
+                                  : (int)(0xFFFFFFFFu - (uint32_t)(klo[s] & 0xFFFFFFFFu));
+                    const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp[s]];
+                    st[s] = (p < A_) ? ((uint32_t)nin[jp[s]] | (wq << 8)) : 0u;
+                }
 #ifdef SW_STAMPS
                 sw_pack_rounds<SW_JPT>(blk, PL, A_, T, G, st, mk, capsp, swp);
 #else
