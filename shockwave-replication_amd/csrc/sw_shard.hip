@@ -286,11 +286,64 @@ __global__ void k_search_init(unsigned long long* sr, unsigned long long lo, uns
     if (threadIdx.x == 0) { sr[0] = lo; sr[1] = hi; sr[2] = (unsigned long long)bud; sr[3] = 0; }
 }
 
+/* One swc_search step on a search state x = (lo, hi, budget, rounds) from
+ * the all-reduced bins of the round that probed it: counts cnt[i] =
+ * Σ_{b > i} bins[b]; the first i with cnt ≤ budget closes the bracket.  One
+ * wave: lane i loads bins[i + 1], a shuffle suffix scan forms cnt[i], a
+ * ballot finds the first i.  Returns the new state in lane 0's out (a
+ * closed bracket is left as it is). */
+__device__ __forceinline__ void search_step_wave(const unsigned long long* x, const long long* bins,
+                                                 unsigned long long* out) {
+    const uint64_t lo = x[0], hi = x[1];
+    const int64_t bud = (int64_t)x[2];
+    const SearchPts q = search_pts(lo, hi);
+    const int i = lane_id();
+    if (q.K == 0) {
+        if (i < 4) out[i] = x[i];
+        return;
+    }
+    int64_t cnt = (i < q.K) ? (int64_t)bins[i + 1] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t v = __shfl_down(cnt, o, 64);
+        cnt += (i + o < 64) ? v : 0;
+    }
+    const uint64_t ok = __ballot(i < q.K && cnt <= bud);
+    if (i == 0) {
+        uint64_t nlo = lo, nhi = hi;
+        if (ok) {
+            const int f = __builtin_ctzll(ok);
+            nhi = search_pt(lo, q, f);
+            if (f > 0) nlo = search_pt(lo, q, f - 1) + 1u;
+        } else {
+            nlo = search_pt(lo, q, q.K - 1) + 1u;
+        }
+        out[0] = nlo;
+        out[1] = nhi;
+        out[2] = x[2];
+        out[3] = x[3] + 1;
+    }
+}
+
+/* Round r of the chained search: first the step of round r − 1 (its
+ * all-reduced bins prev, its state xin) — every block computes it, block 0
+ * stores the result in xout — then the K probes of the new bracket into
+ * S.red.  Fusing the step into the next probe saves a kernel launch per
+ * round; round 0 passes prev = nullptr and probes xin as it is. */
 template <bool LEVEL>
-__global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned long long* sr) {
+__global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned long long* xin,
+                                                   unsigned long long* xout, const long long* prev) {
     __shared__ int32_t bins[SW_SHARD_K + 1];
     __shared__ uint64_t thr[SW_SHARD_K];
-    const uint64_t lo = sr[0], hi = sr[1];
+    __shared__ unsigned long long xs[4];
+    if (prev == nullptr) {
+        if (threadIdx.x < 4) xs[threadIdx.x] = xin[threadIdx.x];
+    } else if (threadIdx.x < 64) {
+        search_step_wave(xin, prev, xs);
+    }
+    __syncthreads();
+    if (prev != nullptr && blockIdx.x == 0 && threadIdx.x < 4) xout[threadIdx.x] = xs[threadIdx.x];
+    const uint64_t lo = xs[0], hi = xs[1];
     const SearchPts q = search_pts(lo, hi);
     if (q.K == 0) return; /* bracket closed: uniform over the grid */
     if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
@@ -302,32 +355,12 @@ __global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned lo
     probe_body<LEVEL>(S, thr, q.K, bins);
 }
 
-/* counts cnt[i] = Σ_{b > i} bins[b]; the first i with cnt ≤ budget closes
- * the bracket (swc_search).  One wave: lane i loads bins[i + 1], a shuffle
- * suffix scan forms cnt[i], a ballot finds the first i. */
+/* the last round's step, in place (one wave) */
 __global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, const long long* bins) {
-    const uint64_t lo = sr[0], hi = sr[1];
-    const int64_t bud = (int64_t)sr[2];
-    const SearchPts q = search_pts(lo, hi);
-    if (q.K == 0) return;
-    const int i = (int)threadIdx.x;
-    int64_t cnt = (i < q.K) ? (int64_t)bins[i + 1] : 0;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t v = __shfl_down(cnt, o, 64);
-        cnt += (i + o < 64) ? v : 0;
-    }
-    const uint64_t ok = __ballot(i < q.K && cnt <= bud);
-    if (i == 0) {
-        if (ok) {
-            const int f = __builtin_ctzll(ok);
-            sr[1] = search_pt(lo, q, f);
-            if (f > 0) sr[0] = search_pt(lo, q, f - 1) + 1u;
-        } else {
-            sr[0] = search_pt(lo, q, q.K - 1) + 1u;
-        }
-        sr[3] += 1;
-    }
+    __shared__ unsigned long long xs[4];
+    search_step_wave(sr, bins, xs);
+    __syncthreads();
+    if (threadIdx.x < 4) sr[threadIdx.x] = xs[threadIdx.x];
 }
 
 __global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b) {
@@ -946,22 +979,33 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
     *rounds = 0;
     *out = lo;
     if (nr == 0) return SW_OK;
-    unsigned long long* sr = S->srch.p;
-    LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sr, (unsigned long long)lo,
+    /* search states X_r alternate between srch[0..3] and srch[4..7]: round r
+     * reads X_{r−1}, applies round r − 1's step and stores X_r (k_probe_dev) */
+    unsigned long long* sb = S->srch.p;
+    /* round r reads round r − 1's slice: keep the nr slices inside one pass of
+     * the ring (a wrap clears the whole ring) */
+    if (S->ring_pos + nr > kRing) S->ring_pos = kRing;
+    LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sb, (unsigned long long)lo,
            (unsigned long long)hi, (long long)bud);
     const unsigned pb = nblk((int64_t)S->NL * S->T);
+    const long long* prev = nullptr;
     for (int r = 0; r < nr; ++r) {
         SH_TRY(zero_red(S, SW_SHARD_K + 1));
+        const unsigned long long* xin = sb + 4 * ((r + 1) & 1); /* X_{r−1} (X_0 for r = 0) */
+        unsigned long long* xout = sb + 4 * (r & 1);
+        if (r == 0) xin = sb;
         if (kind == 0)
             LAUNCH(S, k_probe_dev<false>, dim3(pb > (unsigned)kProbeBlocks ? (unsigned)kProbeBlocks : pb),
-                   dim3(kTB), 0, st, S->dv, sr);
+                   dim3(kTB), 0, st, S->dv, xin, xout, prev);
         else
-            LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, sr);
+            LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev);
         if (S->comm)
             SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
                                      S->comm, st));
-        LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, S->dv.red);
+        prev = S->dv.red;
     }
+    unsigned long long* sr = sb + 4 * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
+    LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev);
     SH_HIP(S, hipMemcpyAsync(S->hx.p, sr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipStreamSynchronize(st));
     unsigned long long v[4];
@@ -1163,7 +1207,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
                S->psend.reserve((size_t)S->P) || S->pall.reserve(M) ||
                S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64) ||
-               S->srch.reserve(4) ||
+               S->srch.reserve(8) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
