@@ -42,6 +42,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
 #include <string>
 #include <vector>
@@ -737,6 +738,18 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_p
     pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
 }
 
+/* Step results to the host without a stream synchronisation: the words are
+ * stored into fine-grained pinned host memory, then a sequence number is
+ * released at system scope; the host spins on it (sw_shard_state::publish).
+ * Plain vector stores (global_store), no scalar-cache writes. */
+__global__ __launch_bounds__(256) void k_publish(const uint32_t* src, uint32_t* dst, int nwords,
+                                                 unsigned long long* flag, unsigned long long seq) {
+    for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n + kTB - 1) / kTB : 1); }
 
 }  // namespace
@@ -745,6 +758,14 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n
 
 struct sw_shard_state {
     sw_handle* h = nullptr;
+    /* step results published by k_publish: fine-grained pinned host memory
+     * (data, then the flag word), its device alias, the last sequence number */
+    uint32_t* pub = nullptr;
+    uint32_t* pub_dev = nullptr;
+    size_t pub_words = 0;
+    unsigned long long* pub_flag = nullptr;
+    unsigned long long* pub_flag_dev = nullptr;
+    unsigned long long pub_seq = 0;
     int32_t rank = 0, world = 1;
     ncclComm_t comm = nullptr;
     bool host_comm = false;
@@ -812,6 +833,52 @@ int host_fail(sw_shard_state* S, const char* what) {
     return SW_ERR_RCCL;
 }
 
+/* Copies `bytes` (a multiple of 4) of device memory to `hout` once the
+ * stream reaches this point: k_publish stores them into pinned host memory
+ * and releases a sequence number, and the host spins on it instead of a
+ * stream synchronisation (the wake-up of hipStreamSynchronize is the larger
+ * part of a host-synchronised step's round trip).  A flag that does not
+ * arrive within 30 s falls back to hipStreamSynchronize, which reports the
+ * failed kernel. */
+int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
+    hipStream_t st = S->h->stream;
+    const size_t words = (bytes + 3) / 4;
+    if (bytes % 4 != 0) return S->h->err = "publish: size not a multiple of 4", SW_ERR_INVALID;
+    if (words > S->pub_words) {
+        if (S->pub) (void)hipHostFree(S->pub);
+        S->pub = nullptr;
+        S->pub_words = 0;
+        const size_t want = words < 2048 ? 2048 : words;
+        SH_HIP(S, hipHostMalloc((void**)&S->pub, want * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        SH_HIP(S, hipHostGetDevicePointer((void**)&S->pub_dev, S->pub, 0));
+        S->pub_words = want;
+    }
+    if (!S->pub_flag) {
+        SH_HIP(S, hipHostMalloc((void**)&S->pub_flag, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        SH_HIP(S, hipHostGetDevicePointer((void**)&S->pub_flag_dev, S->pub_flag, 0));
+        __atomic_store_n(S->pub_flag, 0ull, __ATOMIC_RELEASE);
+        S->pub_seq = 0;
+    }
+    const unsigned long long seq = ++S->pub_seq;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, st, (const uint32_t*)dsrc, S->pub_dev,
+                       (int)words, S->pub_flag_dev, seq);
+    SH_HIP(S, hipGetLastError());
+    auto t0 = std::chrono::steady_clock::now();
+    uint32_t spins = 0;
+    while (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq) {
+        __builtin_ia32_pause();
+        if (((++spins) & 0xFFFFu) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+            SH_HIP(S, hipStreamSynchronize(st));
+            if (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq)
+                return S->h->err = "publish: step result never arrived", SW_ERR_HIP;
+            break;
+        }
+    }
+    memcpy(hout, S->pub, bytes);
+    return SW_OK;
+}
+
 /* In-place all-reduce of n values on the device buffer `dbuf`, copied to
  * `hout`.  op: 0 = sum i64, 1 = max u64, 2 = max f64. */
 int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
@@ -825,9 +892,7 @@ int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
-    SH_HIP(S, hipMemcpyAsync(S->hx.p, dbuf, bytes, hipMemcpyDeviceToHost, st));
-    SH_HIP(S, hipStreamSynchronize(st));
-    memcpy(hout, S->hx.p, bytes);
+    SH_TRY(publish(S, dbuf, bytes, hout));
     if (S->world > 1 && S->host_comm) {
         int rc = op == 0 ? S->hc.allreduce_sum_i64(S->hc.ctx, (int64_t*)hout, n)
                : op == 1 ? S->hc.allreduce_max_u64(S->hc.ctx, (uint64_t*)hout, n)
@@ -853,12 +918,7 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
         } else {
             SH_NCCL(S, ncclAllGather(dsend, drecv, bytes, ncclUint8, S->comm, st));
         }
-        if (hrecv) {
-            if (S->hx.reserve(total)) return host_fail(S, "pinned staging");
-            SH_HIP(S, hipMemcpyAsync(S->hx.p, one ? dsend : drecv, total, hipMemcpyDeviceToHost, st));
-            SH_HIP(S, hipStreamSynchronize(st));
-            memcpy(hrecv, S->hx.p, total);
-        }
+        if (hrecv) SH_TRY(publish(S, one ? dsend : drecv, total, hrecv));
         return SW_OK;
     }
     /* host collectives: down, gather, up */
@@ -1006,10 +1066,8 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
     }
     unsigned long long* sr = sb + 4 * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
     LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev);
-    SH_HIP(S, hipMemcpyAsync(S->hx.p, sr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    SH_HIP(S, hipStreamSynchronize(st));
     unsigned long long v[4];
-    memcpy(v, S->hx.p, sizeof(v));
+    SH_TRY(publish(S, sr, sizeof(v), v));
     *out = v[0];
     *rounds = (int32_t)v[3];
     return SW_OK;
@@ -1282,6 +1340,9 @@ void sw_shard_release(sw_handle* h) {
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
+    if (S->pub) (void)hipHostFree(S->pub);
+    if (S->pub_flag) (void)hipHostFree(S->pub_flag);
+    S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
     S->caps.release(); S->hcaps.release(); S->srch.release(); S->skeys.release(); S->sidx.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
