@@ -496,6 +496,9 @@ struct Ctx {
                     int32_t MX, MN;
                     wg = blk.sum32_max_min(wg, mx, mn, MX, MN);
                     passes++;
+#ifdef SW_STAMPS
+                    if (threadIdx.x == 0 && lsp) lsp[7] += 1; /* price probes */
+#endif
                     const bool down = wg <= bud;
 #pragma unroll
                     for (int s = 0; s < SW_JPT; ++s) {
@@ -684,6 +687,9 @@ struct Ctx {
                 uint64_t BMX, BMN;
                 blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
                 passes++;
+#ifdef SW_STAMPS
+                if (threadIdx.x == 0 && lsp) lsp[8] += 1; /* M_lo passes */
+#endif
                 if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
                 else { lo = BMN <= hi ? BMN : hi; Fb = F; }
             }

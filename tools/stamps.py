@@ -40,6 +40,7 @@ def main():
         st = np.zeros(len(batch) * SLOTS, dtype=np.uint64)
         lib.sw_debug_stamps(s.h, st.ctypes.data_as(C.POINTER(C.c_uint64)))
         st = st.reshape(len(batch), SLOTS).astype(np.float64)
+        st_all = st
         pk = st[:, 8:14]
         ls = st[:, 16:23]
         srt = st[:, 15]
@@ -56,7 +57,8 @@ def main():
         print(f"   sorts (all packs): {srt.mean():.0f}; rounds {rounds:.1f}, active tiers {scans:.1f}, "
               f"width-tail reductions {misses:.1f}")
         lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
-        print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)))
+        print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)),
+              f"| price probes {st_all[:, 23].mean():.1f}, M_lo passes {st_all[:, 24].mean():.1f}")
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
             for r, row, prow in list(zip(res, st, pk))[:24]:
                 print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row), "|",
