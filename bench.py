@@ -94,11 +94,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8192,
-                    help="instances per GPU per step (32 per CU: one 512-thread workgroup fits a "
-                         "CU at a time; a launch ends with its most expensive instances running "
-                         "alone, ~0.75 ms, so more instances per launch amortise that tail, "
-                         "DESIGN.md §6)")
+    ap.add_argument("--batch", type=int, default=16384,
+                    help="instances per GPU per step (64 per CU: one 512-thread workgroup fits a "
+                         "CU at a time, and a launch ends with its most expensive instances "
+                         "running on a few CUs, so more instances per launch amortise that tail: "
+                         "1.198M / 1.237M / 1.286M / 1.301M plan-solves/s at 4096 / 8192 / 16384 / "
+                         "32768, profiles/r2_batch_sweep.log, DESIGN.md §6)")
     ap.add_argument("--jobs", type=int, default=900)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--seed", type=int, default=0)
