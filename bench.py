@@ -31,8 +31,8 @@ sys.path.insert(0, PKG)
 import sw_native as sn  # noqa: E402
 import sw_synth as ss  # noqa: E402
 
-HBM_PEAK = 8.0e12
-C4_SEED = 77  # the C4 instance of the sub-record (tests/golden/c4_digest.json)  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+C4_SEED = 77  # the C4 instance of the sub-record (tests/golden/c4_digest.json)
 
 # The result line is the only thing on stdout: libraries (RCCL prints its
 # version banner on communicator init) write to fd 1 directly, so fd 1 is
@@ -113,9 +113,13 @@ def parse():
                     help="sharded C4 solves timed for the c4_sharded sub-record")
     ap.add_argument("--no-c4", dest="no_c4", action="store_true",
                     help="skip the sharded C4 sub-record of the default line")
+    ap.add_argument("--c5-steps", dest="c5_steps", type=int, default=20,
+                    help="sweeps timed for the c5_sweep sub-record")
+    ap.add_argument("--no-c5", dest="no_c5", action="store_true",
+                    help="skip the C5 sweep sub-record of the default line")
     ap.add_argument("--no-legs", dest="no_legs", action="store_true",
                     help="profiling runs: skip the host-boundary / single-instance / sustained "
-                         "legs and the C4 sub-record")
+                         "legs and the C4 / C5 sub-records")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -341,8 +345,12 @@ def main():
             "speedup_vs_cpu": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }
         line.update(extra)
+    if not (args.no_c5 or args.no_legs):
+        c5 = guarded(c5_leg, "c5_sweep", args, world, rank, local, dist, line)
+        if line is not None:
+            line["c5_sweep"] = c5
     if not (args.no_c4 or args.no_legs):
-        c4 = c4_leg_guarded(args, world, rank, local, dist, line)
+        c4 = guarded(c4_leg, "c4_sharded", args, world, rank, local, dist, line)
         if line is not None:
             line["c4_sharded"] = c4
     # the CPU leg runs last: the host-synchronised C4 controller timed after
@@ -361,37 +369,124 @@ def main():
         dist.destroy_process_group()
 
 
-C4_BUDGET_S = 90.0
+LEG_BUDGET_S = 90.0
 
 
-def c4_leg_guarded(args, world, rank, local, dist, line):
-    """Runs the C4 sub-record so that it can never cost the headline line.
+def guarded(leg, key, args, world, rank, local, dist, line):
+    """Runs a sub-record leg (C4, C5) so that it can never cost the headline line.
 
     An exception on a rank is reported in the sub-record.  A rank that stops
-    answering leaves its peers blocked inside an RCCL collective, which no
+    answering leaves its peers blocked inside a collective, which no
     exception reaches: a watchdog thread then prints the headline line with
-    the C4 failure (rank 0) and ends the process after C4_BUDGET_S."""
+    the failure (rank 0) and ends the process after LEG_BUDGET_S."""
     import threading
 
     done = threading.Event()
 
     def watchdog():
-        if done.wait(C4_BUDGET_S):
+        if done.wait(LEG_BUDGET_S):
             return
         if line is not None:
-            line["c4_sharded"] = {"error": f"no result within {C4_BUDGET_S:g} s on rank {rank} "
-                                           f"(a peer stopped inside a collective)"}
+            line[key] = {"error": f"no result within {LEG_BUDGET_S:g} s on rank {rank} "
+                                  f"(a peer stopped inside a collective)"}
             emit(line)
         sys.stderr.flush()
         os._exit(0)
 
     threading.Thread(target=watchdog, daemon=True).start()
     try:
-        return c4_leg(args, world, rank, local, dist)
+        return leg(args, world, rank, local, dist)
     except Exception as e:  # reported in the line, never hidden
         return {"error": f"rank {rank}: {e!r}"}
     finally:
         done.set()
+
+
+C5_INSTANCES = 512
+C5_SEED0 = 5_000_000
+
+
+def c5_share(probs, world, rank):
+    """Rank `rank`'s instances of the C5 sweep: sweep_problems cycles through
+    the four cluster sizes, so each consecutive group of four holds one
+    instance per size; groups go round-robin to the ranks, and every rank
+    gets the same number of instances of each size (512 / 4 / N)."""
+    ng = 4
+    return [p for i, p in enumerate(probs) if (i // ng) % world == rank]
+
+
+def c5_leg(args, world, rank, local, dist):
+    """The C5 sub-record (BASELINE configs[4]): a FIXED sweep
+    of 512 independent 900-job × 30-round instances, seeds × cluster sizes
+    G ∈ {32, 64, 128, 256} with (k, λ) from the matching scale_*gpus.json
+    (sw_synth.sweep_problems), spread over the N ranks of this run by
+    c5_share (every rank gets the same G mix) in one batched launch per step,
+    no communication.  Total work is fixed, so
+    across the driver's N = 1, 2, 4, 8 runs this is strong scaling; at 512
+    instances one GPU holds two per CU and eight GPUs hold one per CU on a
+    quarter of their CUs, so the sweep ends with its slowest instances (the
+    small-k 128-GPU configuration) either way."""
+    import torch
+
+    probs = ss.sweep_problems(C5_INSTANCES, args.jobs, seed0=C5_SEED0, T_override=args.rounds)
+    mine = c5_share(probs, world, rank)
+    solver = sn.Solver(device=local)
+    solver.upload(mine)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(max(1, args.warmup)):
+        solver.run()
+    res = solver.download()
+    steps = max(1, args.c5_steps)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solver.run()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    solver.close()
+    # mean passes per instance by cluster size, gathered from every rank
+    stats = {}
+    for a, r in zip(mine, res):
+        s = stats.setdefault(int(a.G), [0, 0.0])
+        s[0] += 1
+        s[1] += float(r["iters"])
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        parts = [None] * world
+        dist.all_gather_object(parts, stats)
+    else:
+        parts = [stats]
+    if rank != 0:
+        return None
+    tot = {}
+    for p in parts:
+        for G, (n, it) in p.items():
+            q = tot.setdefault(G, [0, 0.0])
+            q[0] += n
+            q[1] += it
+    return {
+        "metric": "Shockwave plan solves/sec, fixed 512-instance seed x cluster-size sweep over N GPUs",
+        "value": C5_INSTANCES * steps / elapsed,
+        "unit": "plan-solves/s",
+        "ms_per_sweep": elapsed / steps * 1e3,
+        "steps": steps,
+        "scaling": "strong",
+        "config": {"workload": f"C5: {C5_INSTANCES} instances of {args.jobs} jobs x {args.rounds} "
+                               f"rounds, G in (32, 64, 128, 256) with their scale_*gpus.json (k, "
+                               f"lambda); {len(mine)} per rank, one launch per rank per step",
+                   "instances": C5_INSTANCES, "jobs": args.jobs, "rounds": args.rounds,
+                   "ranks": world},
+        "passes_per_instance_by_G": {str(G): it / n for G, (n, it) in sorted(tot.items())},
+    }
 
 
 def boundary_legs(args, solver, batch, results, local):

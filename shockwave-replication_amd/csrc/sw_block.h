@@ -18,13 +18,17 @@
 #define SW_BLOCK 512
 #define SW_WAVES (SW_BLOCK / 64)
 
-struct sw_xchg {
-    int64_t i[2][SW_WAVES][2];
-    double d[2][SW_WAVES][2];
-    uint64_t u[2][SW_WAVES];
-    uint64_t u2[2][SW_WAVES][2];
-    int32_t s[2][SW_WAVES];
+/* NW waves per workgroup: SW_WAVES for the plan kernel; the sharded
+ * engine's placement also runs a 1024-thread (16-wave) round loop */
+template <int NW>
+struct sw_xchg_t {
+    int64_t i[2][NW][2];
+    double d[2][NW][2];
+    uint64_t u[2][NW];
+    uint64_t u2[2][NW][2];
+    int32_t s[2][NW];
 };
+using sw_xchg = sw_xchg_t<SW_WAVES>;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -210,8 +214,9 @@ __device__ __forceinline__ double wave_dettree(double x) {
     return x;
 }
 
-struct sw_blk {
-    sw_xchg* X;
+template <int NW>
+struct sw_blk_t {
+    sw_xchg_t<NW>* X;
     int par;
 
     __device__ __forceinline__ void flip() { par ^= 1; }
@@ -222,7 +227,7 @@ struct sw_blk {
         __syncthreads();
         int32_t t = 0;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) t += X->s[par][w];
+        for (int w = 0; w < NW; ++w) t += X->s[par][w];
         flip();
         return t;
     }
@@ -233,7 +238,7 @@ struct sw_blk {
         __syncthreads();
         int32_t t = X->s[par][0];
 #pragma unroll
-        for (int w = 1; w < SW_WAVES; ++w) t = X->s[par][w] < t ? X->s[par][w] : t;
+        for (int w = 1; w < NW; ++w) t = X->s[par][w] < t ? X->s[par][w] : t;
         flip();
         return t;
     }
@@ -246,7 +251,7 @@ struct sw_blk {
         __syncthreads();
         int64_t t = 0;
 #pragma unroll
-        for (int k = 0; k < SW_WAVES; ++k) t += X->i[par][k][0];
+        for (int k = 0; k < NW; ++k) t += X->i[par][k][0];
         flip();
         return t;
     }
@@ -258,7 +263,7 @@ struct sw_blk {
         __syncthreads();
         int64_t ta = 0, tb = 0;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) { ta += X->i[par][w][0]; tb += X->i[par][w][1]; }
+        for (int w = 0; w < NW; ++w) { ta += X->i[par][w][0]; tb += X->i[par][w][1]; }
         flip();
         ra = ta;
         rb = tb;
@@ -270,7 +275,7 @@ struct sw_blk {
         __syncthreads();
         uint64_t m = 0;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) m = X->u[par][w] > m ? X->u[par][w] : m;
+        for (int w = 0; w < NW; ++w) m = X->u[par][w] > m ? X->u[par][w] : m;
         flip();
         return m;
     }
@@ -281,7 +286,7 @@ struct sw_blk {
         __syncthreads();
         double m = X->d[par][0][0];
 #pragma unroll
-        for (int w = 1; w < SW_WAVES; ++w) m = X->d[par][w][0] > m ? X->d[par][w][0] : m;
+        for (int w = 1; w < NW; ++w) m = X->d[par][w][0] > m ? X->d[par][w][0] : m;
         flip();
         return m;
     }
@@ -301,7 +306,7 @@ struct sw_blk {
         int64_t t = 0;
         uint64_t a = 0, b = ~0ull;
 #pragma unroll
-        for (int k = 0; k < SW_WAVES; ++k) {
+        for (int k = 0; k < NW; ++k) {
             t += X->i[par][k][0];
             a = X->u2[par][k][0] > a ? X->u2[par][k][0] : a;
             b = X->u2[par][k][1] < b ? X->u2[par][k][1] : b;
@@ -327,7 +332,7 @@ struct sw_blk {
         __syncthreads();
         int32_t t = 0, a = 0, b = 0x7FFFFFFF;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) {
+        for (int w = 0; w < NW; ++w) {
             t += (int32_t)X->i[par][w][0];
             const uint64_t p = (uint64_t)X->i[par][w][1];
             const int32_t pm = (int32_t)(p >> 32), pn = (int32_t)(uint32_t)p;
@@ -346,15 +351,15 @@ struct sw_blk {
         m = wave_max_f64(m);
         if (lane_id() == 0) { X->d[par][wave_id()][0] = v; X->d[par][wave_id()][1] = m; }
         __syncthreads();
-        double s[SW_WAVES];
+        double s[NW];
         double mm = X->d[par][0][1];
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) {
+        for (int w = 0; w < NW; ++w) {
             s[w] = X->d[par][w][0];
             mm = X->d[par][w][1] > mm ? X->d[par][w][1] : mm;
         }
 #pragma unroll
-        for (int h = SW_WAVES / 2; h >= 1; h >>= 1)
+        for (int h = NW / 2; h >= 1; h >>= 1)
 #pragma unroll
             for (int i = 0; i < h; ++i) s[i] = s[i] + s[i + h];
         flip();
@@ -375,7 +380,7 @@ struct sw_blk {
         __syncthreads();
         int32_t base = 0, tot = 0;
 #pragma unroll
-        for (int w = 0; w < SW_WAVES; ++w) {
+        for (int w = 0; w < NW; ++w) {
             int32_t t = X->s[par][w];
             base += (w < wave_id()) ? t : 0;
             tot += t;
@@ -385,3 +390,4 @@ struct sw_blk {
         return base + x - v;
     }
 };
+using sw_blk = sw_blk_t<SW_WAVES>;

@@ -84,8 +84,8 @@ __device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int 
 
 /* caps: per-round capacity in LDS (nullptr = G every round) — the class-wise
  * P2 repack, where positions carry unit widths */
-template <int E>
-__device__ __forceinline__ void sw_pack_rounds(sw_blk& blk, sw_pack_lds* L, int A, int T, int G,
+template <int E, class BLK>
+__device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, int T, int G,
                                                uint32_t (&st)[E], uint64_t (&mk)[E],
                                                const int32_t* caps = nullptr,
                                                uint64_t* swp = nullptr) {

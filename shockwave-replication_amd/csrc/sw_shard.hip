@@ -27,7 +27,8 @@
  *   k_probe    thread per (job, round) item: one binary search over the ≤63
  *        ascending thresholds, an LDS histogram, a suffix sum on the host —
  *        K price/level probes per pass (K-ary search)
- *   k_assign   one workgroup: the job-ordered tie group as a block scan
+ *   k_assign   thread per job: the job-ordered tie group, block offsets
+ *        from k_take's per-block tie sums plus a block scan
  *   k_eval_jobs / k_eval_lanes   per-job values (thread per job), then one
  *        workgroup sums each deterministic-sum lane left to right (sw_detsum's
  *        chunks), so the gathered lanes reproduce the single-instance sums
@@ -86,6 +87,7 @@ struct ShardDev {
     int32_t* l;
     int32_t* taken;
     int32_t* tie; /* w·(count(key ≥ ρ) − taken), stored by k_take */
+    long long* tieblk; /* Σ tie per k_take block (k_assign's offsets) */
     double* xa;   /* per-job values of the last reduction (two rows of NL) */
     int32_t* arr[SW_A_COUNT];
     uint64_t* y[SW_Y_COUNT];
@@ -399,38 +401,55 @@ __global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
     }
     red_add(S.red + 0, wt);
     red_add(S.red + 1, tie);
+    /* this block's tie weight, for k_assign's block offsets */
+    __shared__ long long ws[kTB / 64];
+    const long long bt = wave_sum(tie);
+    if (lane_id() == 0) ws[wave_id()] = bt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long s = 0;
+        for (int w = 0; w < kTB / 64; ++w) s += ws[w];
+        S.tieblk[blockIdx.x] = s;
+    }
 }
 
-/* tie group in job order (twin: the excl loop of select_level): one
- * workgroup walks the jobs in coalesced tiles of SW_BLOCK, a block scan per
- * tile, the running prefix carried across tiles */
-__global__ __launch_bounds__(SW_BLOCK) void k_assign(ShardDev S, long long rem, long long excl0) {
-    __shared__ long long wsum[2][SW_WAVES];
-    long long carry = excl0, used = 0;
-    int par = 0;
-    for (int base = 0; base < S.NL; base += SW_BLOCK, par ^= 1) {
-        const int i = base + (int)threadIdx.x;
-        const long long t = i < S.NL ? (long long)S.tie[i] : 0;
-        const long long inc = wave_incscan(t);
-        if (lane_id() == 63) wsum[par][wave_id()] = inc;
-        __syncthreads();
-        long long before = 0, tot = 0;
-        for (int w = 0; w < SW_WAVES; ++w) {
-            before += w < wave_id() ? wsum[par][w] : 0;
-            tot += wsum[par][w];
-        }
-        if (i < S.NL) {
-            const long long excl = carry + before + inc - t;
-            const long long wj = S.jc[i].w;
-            const int tie = (int)(t / wj);
-            int tt;
-            if (excl + t <= rem) tt = tie;
-            else if (excl <= rem) tt = (int)((rem - excl) / wj);
-            else tt = 0;
-            S.arr[SW_A_N][i] = S.l[i] + S.taken[i] + tt;
-            used += wj * tt;
-        }
-        carry += tot;
+/* tie group in job order (twin: the excl loop of select_level): thread per
+ * job, the grid of k_take.  Block b's offset is excl0 plus the tie weights
+ * k_take summed for blocks 0 … b−1, then a block scan: the same integer
+ * prefix as a walk over the jobs in order, without one workgroup walking
+ * them all. */
+__global__ __launch_bounds__(kTB) void k_assign(ShardDev S, long long rem, long long excl0) {
+    __shared__ long long ws[kTB / 64];
+    __shared__ long long boff;
+    long long pb = 0;
+    for (int b = (int)threadIdx.x; b < (int)blockIdx.x; b += kTB) pb += S.tieblk[b];
+    pb = wave_sum(pb);
+    if (lane_id() == 0) ws[wave_id()] = pb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long s = excl0;
+        for (int w = 0; w < kTB / 64; ++w) s += ws[w];
+        boff = s;
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    const long long t = i < S.NL ? (long long)S.tie[i] : 0;
+    const long long inc = wave_incscan(t);
+    if (lane_id() == 63) ws[wave_id()] = inc;
+    __syncthreads();
+    long long before = boff;
+    for (int w = 0; w < wave_id(); ++w) before += ws[w];
+    long long used = 0;
+    if (i < S.NL) {
+        const long long excl = before + inc - t;
+        const long long wj = S.jc[i].w;
+        const int tie = (int)(t / wj);
+        int tt;
+        if (excl + t <= rem) tt = tie;
+        else if (excl <= rem) tt = (int)((rem - excl) / wj);
+        else tt = 0;
+        S.arr[SW_A_N][i] = S.l[i] + S.taken[i] + tt;
+        used = wj * tt;
     }
     red_add(S.red + 0, used);
 }
@@ -675,10 +694,10 @@ __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, cons
 /* the round loop over the global order; writes this rank's rows */
 /* capsd: per-round capacities of the class-wise repack (nullptr = G); then
  * only the entries' rows are written, every other job is left untouched */
-template <int E>
+template <int E, class BLK>
 __device__ __forceinline__ void pack_rounds_body(const ShardDev& S, const sw_pack_ent* all, int A,
                                                  const int32_t* order, uint64_t* ydst, int32_t* pdst,
-                                                 const int32_t* capsd, sw_blk& blk, sw_pack_lds* PL,
+                                                 const int32_t* capsd, BLK& blk, sw_pack_lds* PL,
                                                  const int32_t* capsL) {
     const int tid = threadIdx.x;
     uint32_t st[E];
@@ -714,27 +733,31 @@ __device__ __forceinline__ void pack_rounds_body(const ShardDev& S, const sw_pac
  * 3/8 of a C4 instance's jobs) take positions, and every pass of the loop
  * walks all E.  So the host launches the variant for M and, when M is large,
  * a smaller one too; each counts the active entries A and runs only when
- * alo < A ≤ E·SW_BLOCK (one runs, the other returns at once).  Separate
- * kernels keep each variant's registers to its own E. */
-template <int E>
-__global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
-                                                          int64_t M, const int32_t* order,
-                                                          uint64_t* ydst, int32_t* pdst,
-                                                          const int32_t* capsd, int alo) {
-    __shared__ sw_xchg X;
+ * alo < A ≤ E·NT (one runs, the other returns at once).  Separate kernels
+ * keep each variant's registers to its own E.  NT threads per workgroup:
+ * 1,024 threads with 4 positions each (4 waves per SIMD, 67 VGPRs) placed
+ * C4's 3,748 active jobs in 198 µs against 172 µs for 512 threads with 8
+ * (DESIGN.md §6.1): the 16-wave block reductions cost more than the shorter
+ * walks save, so every variant runs SW_BLOCK threads. */
+template <int E, int NT>
+__global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
+                                                    int64_t M, const int32_t* order,
+                                                    uint64_t* ydst, int32_t* pdst,
+                                                    const int32_t* capsd, int alo) {
+    __shared__ sw_xchg_t<NT / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
-    sw_blk blk;
+    sw_blk_t<NT / 64> blk;
     blk.X = &X;
     blk.par = 0;
     const int tid = threadIdx.x;
     if (capsd && tid < S.T) capsL[tid] = capsd[tid];
     int act = 0;
-    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[e].st != 0;
+    for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
-    if (A <= alo || A > E * SW_BLOCK) return; /* the other variant places these */
+    if (A <= alo || A > E * NT) return; /* the other variant places these */
     if (!capsd)
-        for (int i = tid; i < S.NL; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
+        for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
     pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
 }
 
@@ -783,7 +806,7 @@ struct sw_shard_state {
     DevBuf<float> keys;
     DevBuf<uint64_t> y[SW_Y_COUNT];
     DevBuf<uint8_t> plan;
-    DevBuf<long long> red;
+    DevBuf<long long> red, tieblk;
     DevBuf<sw_pack_ent> psend, pall;
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
@@ -1105,7 +1128,7 @@ int op_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used)
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
     (void)rho; /* k_take stored the tie counts at rho */
-    LAUNCH(S, k_assign, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, (long long)rem,
+    LAUNCH(S, k_assign, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (long long)rem,
            (long long)excl);
     return coll_reduce(S, S->dv.red, 1, 0, used);
 }
@@ -1191,22 +1214,22 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     int32_t* pd = S->arr[pdst].p;
     /* variants by entries M; above 8 positions per thread also the 8-position
      * variant, for instances whose active jobs fit it (k_pack_rounds) */
-#define SW_LAUNCH_PACK(E, ALO)                                                                \
-    LAUNCH(S, k_pack_rounds<E>, dim3(1), dim3(SW_BLOCK), 0, st, dv, S->pall.p, M, S->porder.p, yd, \
+#define SW_LAUNCH_PACK(E, NT, ALO)                                                              \
+    LAUNCH(S, (k_pack_rounds<E, NT>), dim3(1), dim3(NT), 0, st, dv, S->pall.p, M, S->porder.p, yd, \
            pd, capsd, (int)(ALO))
     if (M <= 2 * SW_BLOCK) {
-        SW_LAUNCH_PACK(2, -1);
+        SW_LAUNCH_PACK(2, SW_BLOCK, -1);
     } else if (M <= 8 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, -1);
+        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
     } else if (M <= 20 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, -1);
-        SW_LAUNCH_PACK(20, 8 * SW_BLOCK);
+        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(20, SW_BLOCK, 8 * SW_BLOCK);
     } else if (M <= 32 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, -1);
-        SW_LAUNCH_PACK(32, 8 * SW_BLOCK);
+        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
     } else if (M <= 64 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, -1);
-        SW_LAUNCH_PACK(64, 8 * SW_BLOCK);
+        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
     } else {
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
     }
@@ -1260,6 +1283,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
                S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
                S->l.reserve(NL) || S->taken.reserve(NL) || S->tie.reserve(NL) ||
+               S->tieblk.reserve(nblk((int64_t)NL)) ||
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
@@ -1301,7 +1325,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     }
     sw_pwl_slopes(pr->num_bases, pr->bases, pr->log_bases, v.slope);
     v.jc = S->jc.p; v.keys = S->keys.p; v.p = S->in_p; v.l = S->l.p; v.taken = S->taken.p;
-    v.tie = S->tie.p; v.xa = S->xa.p;
+    v.tie = S->tie.p; v.tieblk = S->tieblk.p; v.xa = S->xa.p;
     for (int a = 0; a < SW_A_COUNT; ++a) v.arr[a] = S->arr[a].p;
     for (int a = 0; a < SW_Y_COUNT; ++a) v.y[a] = S->y[a].p;
     v.plan = S->plan.p; v.planned = S->planned.p; v.red = S->red.p;
@@ -1336,7 +1360,7 @@ void sw_shard_release(sw_handle* h) {
     sw_shard_state* S = h->shard;
     if (S->comm) (void)ncclCommDestroy(S->comm);
     S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
-    S->tie.release(); S->xa.release();
+    S->tie.release(); S->tieblk.release(); S->xa.release();
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
     S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
