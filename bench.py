@@ -353,6 +353,10 @@ def main():
         c4 = guarded(c4_leg, "c4_sharded", args, world, rank, local, dist, line)
         if line is not None:
             line["c4_sharded"] = c4
+        if world > 1:  # the same solve with the peer-memory step transport
+            c4p = guarded(c4_leg_peer, "c4_sharded_peer", args, world, rank, local, dist, line)
+            if line is not None:
+                line["c4_sharded_peer"] = c4p
     # the CPU leg runs last: the host-synchronised C4 controller timed after
     # 15 s of HiGHS on the same core came out 0.25 ms slower per solve
     if rank == 0 and args.cpu_baseline:
@@ -548,7 +552,11 @@ def boundary_legs(args, solver, batch, results, local):
     return out
 
 
-def c4_leg(args, world, rank, local, dist):
+def c4_leg_peer(args, world, rank, local, dist):
+    return c4_leg(args, world, rank, local, dist, transport="peer")
+
+
+def c4_leg(args, world, rank, local, dist, transport="rccl"):
     """The C4 sub-record: ONE 10,000-job × 30-round
     instance with its jobs sharded over the N ranks of this run
     (sw_dist_shard_range), every step's counts / maxima all-reduced and the
@@ -570,6 +578,8 @@ def c4_leg(args, world, rank, local, dist):
     if dist is not None:
         dist.broadcast_object_list(uid, src=0)
     solver.dist_init(uid[0], rank, world)
+    if transport == "peer":  # sw_dist_enable_peer: IPC-mapped regions, one kernel per step
+        solver.dist_enable_peer(a.N)
     shard = sn.DeviceShard(local_arrays, f"cuda:{local}")
 
     def barrier():
@@ -614,7 +624,9 @@ def c4_leg(args, world, rank, local, dist):
         "steps": steps,
         "scaling": "strong",
         "config": {"workload": f"C4: {a.N} jobs x {a.T} rounds, G={a.G}, k={a.k:g}, "
-                               f"lambda={c['lam']:g}; jobs split over {world} ranks, RCCL",
+                               f"lambda={c['lam']:g}; jobs split over {world} ranks, "
+                               + ("RCCL" if transport == "rccl" else
+                                  "peer-memory step transport over xGMI (RCCL for the setup)"),
                    "jobs": a.N, "rounds": a.T, "ranks": world},
         "collective_steps": r["iters"],
         "matches_twin_digest": ok,

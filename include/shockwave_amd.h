@@ -233,6 +233,24 @@ typedef struct sw_host_comm {
 int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int32_t world);
 
 /*
+ * Peer-memory step transport (call after sw_dist_init / sw_dist_init_host,
+ * on every rank, world ≤ SW_PEER_MAX_WORLD): every rank's exchange region is
+ * mapped into every other rank (hipIpcOpenMemHandle; directly for ranks in
+ * the same process), and from then on each step's all-reduce / all-gather is
+ * one kernel on the handle's stream that stores this rank's partial into
+ * every peer's region over xGMI and releases a sequence flag there, waits
+ * (bounded: SW_ERR_RCCL after ~2 s) for every peer's flag in its own region,
+ * and combines in rank order — instead of an RCCL call per step.  The
+ * communicator set up by the init call is used once, to exchange the region
+ * handles.  max_total_jobs bounds the instances (total_jobs) later solves
+ * may pass (the regions are sized from it; larger ones return
+ * SW_ERR_CAPACITY).  World 1 keeps the init call's transport.  Results are
+ * the same bits as with RCCL or host collectives.
+ */
+#define SW_PEER_MAX_WORLD 64
+int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs);
+
+/*
  * Gavel MaxMinFairness allocation for one worker type — the Fig-9 baseline
  * policy of the Shockwave comparison.  Replaces the ECOS solve of
  * policies/max_min_fairness.py:68-93 (MaxMinFairnessPolicy →

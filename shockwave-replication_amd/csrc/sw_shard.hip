@@ -43,6 +43,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <unistd.h>
+
+#include <algorithm>
 #include <chrono>
 #include <new>
 #include <string>
@@ -766,11 +769,98 @@ __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_en
  * released at system scope; the host spins on it (sw_shard_state::publish).
  * Plain vector stores (global_store), no scalar-cache writes. */
 __global__ __launch_bounds__(256) void k_publish(const uint32_t* src, uint32_t* dst, int nwords,
-                                                 unsigned long long* flag, unsigned long long seq) {
+                                                 unsigned long long* flag, unsigned long long seq,
+                                                 const int* xerr) {
     for (int i = threadIdx.x; i < nwords; i += blockDim.x) dst[i] = src[i];
+    /* one word after the data: the peer transport's sticky error (0 if none) */
+    if (threadIdx.x == 0) dst[nwords] = xerr ? (uint32_t)*xerr : 0u;
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* ---- peer-memory step transport (sw_dist_enable_peer) ----------------------
+ * Every rank's exchange region: kXHdr bytes of sequence flags (u64 per source
+ * rank), then two halves (by sequence parity) of W slots.  A collective is one
+ * single-workgroup kernel: this rank's payload is stored into slot `rank` of
+ * the current half of EVERY rank's region (over xGMI for ranks on other GPUs),
+ * a system-scope release of `seq` into each region's flag `rank` follows, then
+ * lane 0 waits for all W flags of its own region to reach `seq` (bounded; a
+ * timeout sets the sticky error word) and the workgroup combines the W slots
+ * in rank order (all-reduce) or leaves them in place (all-gather: the half IS
+ * the gathered array, rank r's block at r·bytes).  Parity halves: a peer can be
+ * one exchange ahead but not two (exchange s + 2 needs this rank's flag s + 1,
+ * released only after this rank consumed s), so no slot is overwritten while
+ * it is read.  The payload is read completely before anything is combined, so
+ * in-place all-reduces are safe. */
+constexpr int kXHdr = 1024;
+constexpr unsigned long long kXTimeout = 200ull * 1000 * 1000; /* wall_clock64 ticks (100 MHz): 2 s */
+
+struct PeerSet {
+    unsigned char* base[SW_PEER_MAX_WORLD];
+};
+
+__global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* src, long long bytes,
+                                              long long half, int rank, int W, unsigned long long seq,
+                                              int op, int n, unsigned char* dst, int* xerr) {
+    const long long off = kXHdr + (long long)(seq & 1ull) * half + (long long)rank * bytes;
+    if ((bytes & 15) == 0 && ((uintptr_t)src & 15) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        const long long n16 = bytes >> 4;
+        for (long long i = threadIdx.x; i < n16; i += 256) {
+            const uint4 v = s4[i];
+            for (int p = 0; p < W; ++p) reinterpret_cast<uint4*>(ps.base[p] + off)[i] = v;
+        }
+    } else {
+        const unsigned long long* s8 = reinterpret_cast<const unsigned long long*>(src);
+        const long long n8 = bytes >> 3;
+        for (long long i = threadIdx.x; i < n8; i += 256) {
+            const unsigned long long v = s8[i];
+            for (int p = 0; p < W; ++p) reinterpret_cast<unsigned long long*>(ps.base[p] + off)[i] = v;
+        }
+    }
+    __threadfence_system();
+    __syncthreads();
+    if ((int)threadIdx.x < W)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(ps.base[threadIdx.x]) + rank, seq,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __shared__ int bad;
+    if (threadIdx.x == 0) {
+        int b = 0;
+        const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(ps.base[rank]);
+        const uint64_t t0 = wall_clock64();
+        for (int sr = 0; sr < W && !b; ++sr)
+            while (__hip_atomic_load(fl + sr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+                if (wall_clock64() - t0 > kXTimeout) { b = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        if (b) atomicExch(xerr, 1);
+        bad = b;
+    }
+    __syncthreads();
+    if (bad || op == 3) return;
+    const unsigned char* mine = ps.base[rank] + kXHdr + (long long)(seq & 1ull) * half;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        if (op == 0) {
+            long long v = 0;
+            for (int sr = 0; sr < W; ++sr) v += reinterpret_cast<const long long*>(mine + sr * bytes)[i];
+            reinterpret_cast<long long*>(dst)[i] = v;
+        } else if (op == 1) {
+            unsigned long long v = 0;
+            for (int sr = 0; sr < W; ++sr) {
+                const unsigned long long x = reinterpret_cast<const unsigned long long*>(mine + sr * bytes)[i];
+                v = x > v ? x : v;
+            }
+            reinterpret_cast<unsigned long long*>(dst)[i] = v;
+        } else {
+            double v = reinterpret_cast<const double*>(mine)[i];
+            for (int sr = 1; sr < W; ++sr) {
+                const double x = reinterpret_cast<const double*>(mine + sr * bytes)[i];
+                v = x > v ? x : v;
+            }
+            reinterpret_cast<double*>(dst)[i] = v;
+        }
+    }
 }
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n + kTB - 1) / kTB : 1); }
@@ -793,6 +883,17 @@ struct sw_shard_state {
     ncclComm_t comm = nullptr;
     bool host_comm = false;
     sw_host_comm hc;
+    /* peer-memory transport (sw_dist_enable_peer): own region, every rank's
+     * region as mapped here, IPC mappings to close, half size, sequence,
+     * sticky device error word, the largest total_jobs the regions fit */
+    bool peer = false;
+    unsigned char* xreg = nullptr;
+    PeerSet ps{};
+    void* opened[SW_PEER_MAX_WORLD] = {};
+    long long xhalf = 0, xslot = 0;
+    unsigned long long xseq = 0;
+    int* xerr = nullptr;
+    int64_t xmax_jobs = 0;
     /* current solve */
     int32_t NL = 0, T = 0;
     int64_t N = 0, off = 0, q = 1, P = 0, LW = 0;
@@ -867,11 +968,11 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
     hipStream_t st = S->h->stream;
     const size_t words = (bytes + 3) / 4;
     if (bytes % 4 != 0) return S->h->err = "publish: size not a multiple of 4", SW_ERR_INVALID;
-    if (words > S->pub_words) {
+    if (words + 1 > S->pub_words) { /* + the transport's error word */
         if (S->pub) (void)hipHostFree(S->pub);
         S->pub = nullptr;
         S->pub_words = 0;
-        const size_t want = words < 2048 ? 2048 : words;
+        const size_t want = words + 1 < 2048 ? 2048 : words + 1;
         SH_HIP(S, hipHostMalloc((void**)&S->pub, want * 4, hipHostMallocMapped | hipHostMallocCoherent));
         SH_HIP(S, hipHostGetDevicePointer((void**)&S->pub_dev, S->pub, 0));
         S->pub_words = want;
@@ -884,7 +985,7 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
     }
     const unsigned long long seq = ++S->pub_seq;
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, st, (const uint32_t*)dsrc, S->pub_dev,
-                       (int)words, S->pub_flag_dev, seq);
+                       (int)words, S->pub_flag_dev, seq, (const int*)S->xerr);
     SH_HIP(S, hipGetLastError());
     auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
@@ -898,8 +999,27 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
             break;
         }
     }
+    if (S->pub[words] != 0u)
+        return S->h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
     memcpy(hout, S->pub, bytes);
     return SW_OK;
+}
+
+/* One peer-transport collective (k_xchg) on the handle's stream. */
+int peer_xchg(sw_shard_state* S, const void* src, size_t bytes, int op, int n, void* dst) {
+    if ((long long)bytes > S->xslot)
+        return S->h->err = "peer exchange: step payload exceeds the region slot", SW_ERR_CAPACITY;
+    if (bytes % 8 != 0) return S->h->err = "peer exchange: size not a multiple of 8", SW_ERR_INVALID;
+    hipLaunchKernelGGL(k_xchg, dim3(1), dim3(256), 0, S->h->stream, S->ps, (const unsigned char*)src,
+                       (long long)bytes, S->xhalf, (int)S->rank, (int)S->world, ++S->xseq, op, n,
+                       (unsigned char*)dst, S->xerr);
+    SH_HIP(S, hipGetLastError());
+    return SW_OK;
+}
+
+/* this rank's view of the last peer all-gather (rank r's block at r·bytes) */
+inline const void* peer_gathered(const sw_shard_state* S) {
+    return S->xreg + kXHdr + (long long)(S->xseq & 1ull) * S->xhalf;
 }
 
 /* In-place all-reduce of n values on the device buffer `dbuf`, copied to
@@ -911,12 +1031,14 @@ int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
      * included (it is the identity there, but the path is the one the
      * multi-GPU solve takes); without one (a single rank never initialised
      * for collectives) it is skipped */
-    if (S->comm) {
+    if (S->peer) {
+        SH_TRY(peer_xchg(S, dbuf, bytes, op, n, dbuf));
+    } else if (S->comm) {
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
     SH_TRY(publish(S, dbuf, bytes, hout));
-    if (S->world > 1 && S->host_comm) {
+    if (S->world > 1 && S->host_comm && !S->peer) {
         int rc = op == 0 ? S->hc.allreduce_sum_i64(S->hc.ctx, (int64_t*)hout, n)
                : op == 1 ? S->hc.allreduce_max_u64(S->hc.ctx, (uint64_t*)hout, n)
                          : S->hc.allreduce_max_f64(S->hc.ctx, (double*)hout, n);
@@ -926,10 +1048,22 @@ int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
 }
 
 /* All-gather `bytes` per rank from dsend into drecv (device, rank order).
- * If hrecv is set, the gathered blocks are also copied to the host. */
-int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes, void* hrecv) {
+ * If hrecv is set, the gathered blocks are also copied to the host.  With the
+ * peer transport the gathered blocks stay in this rank's exchange region:
+ * *dview (if given) receives where they are on the device (drecv otherwise). */
+int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes, void* hrecv,
+                const void** dview = nullptr) {
     hipStream_t st = S->h->stream;
     const size_t total = bytes * (size_t)S->world;
+    if (dview) *dview = drecv;
+    if (S->peer) {
+        SH_TRY(peer_xchg(S, dsend, bytes, 3, 0, nullptr));
+        const void* g = peer_gathered(S);
+        if (dview) *dview = g;
+        else if (!hrecv) SH_HIP(S, hipMemcpyAsync(drecv, g, total, hipMemcpyDeviceToDevice, st));
+        if (hrecv) SH_TRY(publish(S, g, total, hrecv));
+        return SW_OK;
+    }
     if (!S->host_comm) {
         const bool one = !S->comm;
         /* no communicator: the gather is the identity; a gather read back by
@@ -1082,7 +1216,9 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
                    dim3(kTB), 0, st, S->dv, xin, xout, prev);
         else
             LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev);
-        if (S->comm)
+        if (S->peer)
+            SH_TRY(peer_xchg(S, S->dv.red, (size_t)(SW_SHARD_K + 1) * 8, 0, SW_SHARD_K + 1, S->dv.red));
+        else if (S->comm)
             SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
                                      S->comm, st));
         prev = S->dv.red;
@@ -1203,9 +1339,11 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     }
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
            (int)wc, S->psend.p);
-    SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr));
+    const void* gv = nullptr;
+    SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
+    const sw_pack_ent* all = (const sw_pack_ent*)gv;
     const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
-    LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, S->pall.p, M, S->skeys.p,
+    LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, all, M, S->skeys.p,
            S->sidx.p);
     LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
            S->sidx.p, nch, S->porder.p);
@@ -1215,7 +1353,7 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     /* variants by entries M; above 8 positions per thread also the 8-position
      * variant, for instances whose active jobs fit it (k_pack_rounds) */
 #define SW_LAUNCH_PACK(E, NT, ALO)                                                              \
-    LAUNCH(S, (k_pack_rounds<E, NT>), dim3(1), dim3(NT), 0, st, dv, S->pall.p, M, S->porder.p, yd, \
+    LAUNCH(S, (k_pack_rounds<E, NT>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, \
            pd, capsd, (int)(ALO))
     if (M <= 2 * SW_BLOCK) {
         SW_LAUNCH_PACK(2, SW_BLOCK, -1);
@@ -1359,6 +1497,10 @@ void sw_shard_release(sw_handle* h) {
     if (!h || !h->shard) return;
     sw_shard_state* S = h->shard;
     if (S->comm) (void)ncclCommDestroy(S->comm);
+    for (int p = 0; p < SW_PEER_MAX_WORLD; ++p)
+        if (S->opened[p]) (void)hipIpcCloseMemHandle(S->opened[p]);
+    if (S->xreg) (void)hipFree(S->xreg);
+    if (S->xerr) (void)hipFree(S->xerr);
     S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
     S->tie.release(); S->tieblk.release(); S->xa.release();
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
@@ -1431,6 +1573,89 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
 
 }  // extern "C"
 
+/* Region slot bytes for instances up to `jobs` jobs at world W: the largest
+ * step payload — the placement entries (P·24 B), the lane partials
+ * ((2·LW + 2)·8 B), the widths (P·4 B) or a ≤ 128-value all-reduce. */
+static long long peer_slot_bytes(int64_t jobs, int32_t W) {
+    const int64_t q = std::max<int64_t>(1, (jobs + SW_DET_LANES - 1) / SW_DET_LANES);
+    const int64_t LW = SW_DET_LANES / W, P = LW * q;
+    long long b = std::max<long long>({(long long)P * (long long)sizeof(sw_pack_ent), (2 * LW + 2) * 8,
+                                       P * 4, (long long)kRed * 8});
+    return (b + 255) / 256 * 256;
+}
+
+int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
+    if (!h || !h->shard || max_total_jobs < 0) return SW_ERR_INVALID;
+    sw_shard_state* S = h->shard;
+    const int32_t W = S->world;
+    if (W == 1) return SW_OK; /* nothing to exchange: the init call's transport stays */
+    if (W > SW_PEER_MAX_WORLD) return h->err = "peer transport: world exceeds SW_PEER_MAX_WORLD", SW_ERR_INVALID;
+    if (S->peer) return h->err = "peer transport already enabled", SW_ERR_INVALID;
+    if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
+    const long long slot = peer_slot_bytes(max_total_jobs, W);
+    const long long half = slot * W;
+    const size_t bytes = (size_t)kXHdr + 2 * (size_t)half;
+    /* fine-grained device memory: peers write it over xGMI, and this GPU's
+     * L2 must not hold stale copies of those lines */
+    void* reg = nullptr;
+    if (hipExtMallocWithFlags(&reg, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+        (void)hipGetLastError();
+        SH_HIP(S, hipMalloc(&reg, bytes));
+    }
+    S->xreg = (unsigned char*)reg;
+    SH_HIP(S, hipMemset(S->xreg, 0, bytes));
+    SH_HIP(S, hipMalloc((void**)&S->xerr, sizeof(int)));
+    SH_HIP(S, hipMemset(S->xerr, 0, sizeof(int)));
+    SH_HIP(S, hipDeviceSynchronize());
+    /* every rank: {pid, region pointer, IPC handle}, all-gathered on the init
+     * call's collective */
+    struct Rec {
+        long long pid;
+        unsigned long long ptr;
+        hipIpcMemHandle_t ih;
+    };
+    Rec mine;
+    memset(&mine, 0, sizeof(mine));
+    mine.pid = (long long)getpid();
+    mine.ptr = (unsigned long long)(uintptr_t)S->xreg;
+    SH_HIP(S, hipIpcGetMemHandle(&mine.ih, S->xreg));
+    std::vector<Rec> all((size_t)W);
+    if (S->host_comm) {
+        if (S->hc.allgather(S->hc.ctx, &mine, all.data(), (int64_t)sizeof(Rec)))
+            return host_fail(S, "peer handle all-gather");
+    } else if (S->comm) {
+        DevBuf<unsigned char> dsend, drecv;
+        if (dsend.reserve(sizeof(Rec)) || drecv.reserve(sizeof(Rec) * (size_t)W))
+            return h->err = "peer transport: allocation failed", SW_ERR_HIP;
+        SH_HIP(S, hipMemcpy(dsend.p, &mine, sizeof(Rec), hipMemcpyHostToDevice));
+        SH_NCCL(S, ncclAllGather(dsend.p, drecv.p, sizeof(Rec), ncclUint8, S->comm, h->stream));
+        SH_HIP(S, hipStreamSynchronize(h->stream));
+        SH_HIP(S, hipMemcpy(all.data(), drecv.p, sizeof(Rec) * (size_t)W, hipMemcpyDeviceToHost));
+        dsend.release();
+        drecv.release();
+    } else {
+        return h->err = "peer transport: sw_dist_init or sw_dist_init_host first", SW_ERR_INVALID;
+    }
+    for (int32_t p = 0; p < W; ++p) {
+        if (p == S->rank) {
+            S->ps.base[p] = S->xreg;
+        } else if (all[(size_t)p].pid == mine.pid) { /* same process: the pointer itself */
+            S->ps.base[p] = (unsigned char*)(uintptr_t)all[(size_t)p].ptr;
+        } else {
+            void* q = nullptr;
+            SH_HIP(S, hipIpcOpenMemHandle(&q, all[(size_t)p].ih, hipIpcMemLazyEnablePeerAccess));
+            S->opened[p] = q;
+            S->ps.base[p] = (unsigned char*)q;
+        }
+    }
+    S->xslot = slot;
+    S->xhalf = half;
+    S->xseq = 0;
+    S->xmax_jobs = max_total_jobs;
+    S->peer = true;
+    return SW_OK;
+}
+
 namespace {
 int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
                sw_result* res, bool dev) {
@@ -1453,6 +1678,8 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
         hi - lo != local->num_jobs)
         return h->err = "slice does not match sw_dist_shard_range", SW_ERR_INVALID;
     if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
+    if (S->peer && total_jobs > S->xmax_jobs)
+        return h->err = "total_jobs exceeds sw_dist_enable_peer's max_total_jobs", SW_ERR_CAPACITY;
     SH_TRY(prepare(S, local, job_offset, total_jobs, dev, res));
     sw_shard_ops ops;
     ops.ctx = S;
@@ -1486,6 +1713,11 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
                                      h->stream));
     }
     SH_HIP(S, hipStreamSynchronize(h->stream));
+    if (S->peer) { /* a timed-out exchange after the last publish */
+        int e = 0;
+        SH_HIP(S, hipMemcpy(&e, S->xerr, sizeof(int), hipMemcpyDeviceToHost));
+        if (e) return h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+    }
     return rc;
 }
 }  // namespace

@@ -313,7 +313,7 @@ EXPORTED_SYMBOLS = (
     "sw_plan_solve", "sw_plan_solve_batch", "sw_batch_upload", "sw_batch_run",
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
     "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
-    "sw_dist_init_host", "sw_mmf_allocate", "sw_dist_plan_solve_dev",
+    "sw_dist_init_host", "sw_mmf_allocate", "sw_dist_plan_solve_dev", "sw_dist_enable_peer",
 )
 
 
@@ -377,6 +377,8 @@ def load(path: str | None = None):
     lib.sw_dist_shard_range.restype = C.c_int
     lib.sw_dist_init_host.argtypes = [C.c_void_p, C.POINTER(SwHostComm), C.c_int32, C.c_int32]
     lib.sw_dist_init_host.restype = C.c_int
+    lib.sw_dist_enable_peer.argtypes = [C.c_void_p, C.c_int64]
+    lib.sw_dist_enable_peer.restype = C.c_int
     lib.sw_mmf_allocate.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _ip, _dp, _dp, _dp]
     lib.sw_mmf_allocate.restype = C.c_int
     if path is None:
@@ -484,6 +486,13 @@ class Solver:
         self._comm = comm  # keeps the callbacks alive
         self._check(self.lib.sw_dist_init_host(self.h, C.byref(comm.c), int(rank), int(world)),
                     "sw_dist_init_host")
+
+    def dist_enable_peer(self, max_total_jobs: int):
+        """Peer-memory step transport (sw_dist_enable_peer): each step's
+        collective becomes one kernel that writes into the other ranks'
+        IPC-mapped exchange regions over xGMI; after dist_init or
+        dist_init_host, on every rank."""
+        self._check(self.lib.sw_dist_enable_peer(self.h, int(max_total_jobs)), "sw_dist_enable_peer")
 
     def dist_solve(self, local: ProblemArrays, job_offset: int, total_jobs: int) -> dict:
         prob = local.c_problem()

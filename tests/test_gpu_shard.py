@@ -125,3 +125,48 @@ def test_gpu_shard_device_rejects_bad_input(rccl_solver):
     torch.cuda.synchronize()
     r = rccl_solver.dist_solve_dev(shard, 0, a.N)  # the handle recovers
     assert r["rc"] in (0, 1)
+
+
+def test_gpu_shard_peer_transport_two_processes(tmp_path, twin):
+    """sw_dist_enable_peer: two processes on cuda:0 (gloo only for the setup),
+    every step's all-reduce / all-gather one k_xchg kernel writing into the
+    other process's IPC-mapped exchange region; the result must be the
+    single-instance twin's, bit for bit, C4 shape included."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    c = ss.C4
+    cases = [CASES[1], CASES[6], CASES[7], (13, c["N"], c["G"], c["T"], c["k"], c["lam"])]
+    cj = tmp_path / "cases.json"
+    cj.write_text(json.dumps([list(x) for x in cases]))
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "peer_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", str(port), str(tmp_path), str(cj)])
+             for r in range(2)]
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=150))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(None)
+    assert rcs == [0, 0], rcs
+    for ci, case in enumerate(cases):
+        seed, N, G, T, k, lam = case
+        a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+        parts = []
+        for r in range(2):
+            z = np.load(tmp_path / f"c{ci}_r{r}.npz")
+            res = {key: float(v) for key, v in zip(("objective", "utility", "makespan",
+                                                      "p2_objective", "bound"), z["scal"])}
+            res.update(rc=int(z["meta"][0]), status=int(z["meta"][1]), iters=int(z["meta"][2]),
+                       plan=z["plan"], planned_rounds=z["cnt"])
+            parts.append((int(z["lo"]), int(z["hi"]), res))
+        rs = assemble(a, parts)
+        check_plan_valid(a, rs)
+        assert_same_as_single(rs, twin.solve(a), f"peer W=2 {case}")
