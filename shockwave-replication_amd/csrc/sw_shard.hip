@@ -800,9 +800,15 @@ struct PeerSet {
     unsigned char* base[SW_PEER_MAX_WORLD];
 };
 
+/* hdst / hflag (optional): the combined result (all-reduce) or the gathered
+ * half (all-gather) also goes to pinned host memory, followed by the error
+ * word and a system-scope release of hseq — the host-synchronised steps then
+ * need no k_publish launch of their own */
 __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* src, long long bytes,
                                               long long half, int rank, int W, unsigned long long seq,
-                                              int op, int n, unsigned char* dst, int* xerr) {
+                                              int op, int n, unsigned char* dst, int* xerr,
+                                              uint32_t* hdst, unsigned long long* hflag,
+                                              unsigned long long hseq) {
     const long long off = kXHdr + (long long)(seq & 1ull) * half + (long long)rank * bytes;
     if ((bytes & 15) == 0 && ((uintptr_t)src & 15) == 0) {
         const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -838,9 +844,8 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
         bad = b;
     }
     __syncthreads();
-    if (bad || op == 3) return;
     const unsigned char* mine = ps.base[rank] + kXHdr + (long long)(seq & 1ull) * half;
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = threadIdx.x; i < ((bad || op == 3) ? 0 : n); i += 256) {
         if (op == 0) {
             long long v = 0;
             for (int sr = 0; sr < W; ++sr) v += reinterpret_cast<const long long*>(mine + sr * bytes)[i];
@@ -860,6 +865,17 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
             }
             reinterpret_cast<double*>(dst)[i] = v;
         }
+    }
+    if (hdst) {
+        __syncthreads(); /* the combine is complete */
+        const uint32_t* from = reinterpret_cast<const uint32_t*>(op == 3 ? mine : dst);
+        const int words = op == 3 ? (int)((long long)W * bytes / 4) : 2 * n;
+        if (!bad)
+            for (int i = threadIdx.x; i < words; i += 256) hdst[i] = from[i];
+        if (threadIdx.x == 0) hdst[words] = bad ? 1u : 0u;
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(hflag, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -964,10 +980,8 @@ int host_fail(sw_shard_state* S, const char* what) {
  * part of a host-synchronised step's round trip).  A flag that does not
  * arrive within 30 s falls back to hipStreamSynchronize, which reports the
  * failed kernel. */
-int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
-    hipStream_t st = S->h->stream;
-    const size_t words = (bytes + 3) / 4;
-    if (bytes % 4 != 0) return S->h->err = "publish: size not a multiple of 4", SW_ERR_INVALID;
+/* pinned buffers for `words` result words + the error word */
+int publish_reserve(sw_shard_state* S, size_t words) {
     if (words + 1 > S->pub_words) { /* + the transport's error word */
         if (S->pub) (void)hipHostFree(S->pub);
         S->pub = nullptr;
@@ -983,10 +997,12 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
         __atomic_store_n(S->pub_flag, 0ull, __ATOMIC_RELEASE);
         S->pub_seq = 0;
     }
-    const unsigned long long seq = ++S->pub_seq;
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, st, (const uint32_t*)dsrc, S->pub_dev,
-                       (int)words, S->pub_flag_dev, seq, (const int*)S->xerr);
-    SH_HIP(S, hipGetLastError());
+    return SW_OK;
+}
+
+/* spin until sequence number seq is released, then copy the words out */
+int publish_wait(sw_shard_state* S, unsigned long long seq, size_t words, size_t bytes, void* hout) {
+    hipStream_t st = S->h->stream;
     auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
     while (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq) {
@@ -1005,15 +1021,36 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
     return SW_OK;
 }
 
+int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
+    const size_t words = (bytes + 3) / 4;
+    if (bytes % 4 != 0) return S->h->err = "publish: size not a multiple of 4", SW_ERR_INVALID;
+    SH_TRY(publish_reserve(S, words));
+    const unsigned long long seq = ++S->pub_seq;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, S->h->stream, (const uint32_t*)dsrc,
+                       S->pub_dev, (int)words, S->pub_flag_dev, seq, (const int*)S->xerr);
+    SH_HIP(S, hipGetLastError());
+    return publish_wait(S, seq, words, bytes, hout);
+}
+
 /* One peer-transport collective (k_xchg) on the handle's stream. */
-int peer_xchg(sw_shard_state* S, const void* src, size_t bytes, int op, int n, void* dst) {
+/* hout (optional): the result also comes to the host (fused publish) */
+int peer_xchg(sw_shard_state* S, const void* src, size_t bytes, int op, int n, void* dst,
+              void* hout = nullptr) {
     if ((long long)bytes > S->xslot)
         return S->h->err = "peer exchange: step payload exceeds the region slot", SW_ERR_CAPACITY;
     if (bytes % 8 != 0) return S->h->err = "peer exchange: size not a multiple of 8", SW_ERR_INVALID;
+    const size_t obytes = op == 3 ? bytes * (size_t)S->world : (size_t)n * 8;
+    unsigned long long hseq = 0;
+    if (hout) {
+        SH_TRY(publish_reserve(S, obytes / 4));
+        hseq = ++S->pub_seq;
+    }
     hipLaunchKernelGGL(k_xchg, dim3(1), dim3(256), 0, S->h->stream, S->ps, (const unsigned char*)src,
                        (long long)bytes, S->xhalf, (int)S->rank, (int)S->world, ++S->xseq, op, n,
-                       (unsigned char*)dst, S->xerr);
+                       (unsigned char*)dst, S->xerr, hout ? S->pub_dev : nullptr,
+                       hout ? S->pub_flag_dev : nullptr, hseq);
     SH_HIP(S, hipGetLastError());
+    if (hout) return publish_wait(S, hseq, obytes / 4, obytes, hout);
     return SW_OK;
 }
 
@@ -1031,9 +1068,8 @@ int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
      * included (it is the identity there, but the path is the one the
      * multi-GPU solve takes); without one (a single rank never initialised
      * for collectives) it is skipped */
-    if (S->peer) {
-        SH_TRY(peer_xchg(S, dbuf, bytes, op, n, dbuf));
-    } else if (S->comm) {
+    if (S->peer) return peer_xchg(S, dbuf, bytes, op, n, dbuf, hout);
+    if (S->comm) {
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
@@ -1057,11 +1093,10 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
     const size_t total = bytes * (size_t)S->world;
     if (dview) *dview = drecv;
     if (S->peer) {
-        SH_TRY(peer_xchg(S, dsend, bytes, 3, 0, nullptr));
+        SH_TRY(peer_xchg(S, dsend, bytes, 3, 0, nullptr, hrecv));
         const void* g = peer_gathered(S);
         if (dview) *dview = g;
         else if (!hrecv) SH_HIP(S, hipMemcpyAsync(drecv, g, total, hipMemcpyDeviceToDevice, st));
-        if (hrecv) SH_TRY(publish(S, g, total, hrecv));
         return SW_OK;
     }
     if (!S->host_comm) {
