@@ -1159,7 +1159,7 @@ int op_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
     uint64_t mx[4];
     SH_TRY(coll_reduce(S, S->dv.red, 4, 1, mx));
     if (mx[2]) return S->h->err = "invalid problem (per-job inputs)", SW_ERR_INVALID; /* every rank */
-    if (S->host_comm && S->world > 1) { /* kernels read A from red[0] */
+    if (S->host_comm && S->world > 1 && !S->peer) { /* kernels read A from red[0] */
         memcpy(S->hx.p, mx, 16);
         SH_HIP(S, hipMemcpyAsync(S->dv.red, S->hx.p, 16, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipStreamSynchronize(st));
@@ -1734,7 +1734,7 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.pack = op_pack;
     ops.class_caps = op_class_caps;
     ops.pack_class = op_pack_class;
-    ops.search = S->host_comm ? nullptr : op_search;
+    ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,
                             &res->p2_objective, &res->bound, &res->iters, &res->status);
