@@ -140,6 +140,7 @@ struct Ctx {
 #endif
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
     uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
+    uint8_t* tiecur; /* the take pass's tie counts, read by the tie group */
     uint64_t *ycur, *ybest, *y2;
     /* packer: transposed position state, masks, order, sort buffers */
     uint32_t* pst;
@@ -211,24 +212,6 @@ struct Ctx {
         }
     }
 
-    /* #{n ∈ [0, hi) : g(n) > x} for the nonincreasing g — the first n with
-     * g(n) ≤ x, by binary search (twin: the counting loops). */
-    __device__ __forceinline__ int g_count_gt(const sw_jobc& c, int hi, double x) const {
-        int lo = 0;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sw_g(&c, mid) > x) lo = mid + 1; else hi = mid;
-        }
-        return lo;
-    }
-    __device__ __forceinline__ int g_count_ge(const sw_jobc& c, int hi, double x) const {
-        int lo = 0;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sw_g(&c, mid) >= x) lo = mid + 1; else hi = mid;
-        }
-        return lo;
-    }
     /* twin: lforce */
     __device__ __forceinline__ int lforce(int j, int s, double M) const {
         double gi, gb;
@@ -270,6 +253,33 @@ struct Ctx {
                 break;
             }
             gi = gp;
+            --n;
+        }
+        return n;
+    }
+    /* #{n ≤ Tj : g(n) > x} (GE: ≥ x) — the first n ∈ [0, Tj] where the
+     * monotone predicate fails, found like lforce_g: guessed from the linear
+     * part of g, settled by an exact walk (the binary search's answer in
+     * two or three evaluations of g instead of five or six) */
+    template <bool GE>
+    __device__ __forceinline__ int g_cnt(int j, int s, double x) const {
+        const sw_jobc c = jc(j, s);
+        const int tj = Tj(j, s);
+        const double gt = sw_g(&c, tj);
+        if (GE ? (gt >= x) : (gt > x)) return tj + 1;
+        const double xx = (c.R - x) * inv_delta;
+        int n = xx <= 0.0 ? 0 : (xx >= (double)tj ? tj : (int)ceil(xx));
+        double gn = n == tj ? gt : sw_g(&c, n);
+        if (GE ? (gn >= x) : (gn > x)) {
+            do {
+                ++n;
+                gn = n == tj ? gt : sw_g(&c, n);
+            } while (GE ? (gn >= x) : (gn > x));
+            return n;
+        }
+        while (n > 0) {
+            const double gp = sw_g(&c, n - 1);
+            if (GE ? (gp >= x) : (gp > x)) break;
             --n;
         }
         return n;
@@ -540,9 +550,11 @@ struct Ctx {
             int32_t tie_l = 0;
             for_jobs([&](int j, int s) {
                 const int tk = cnt<false>(j, s, rho, lcur[j]);
+                const int tie = cnt<true>(j, s, rho, lcur[j]) - tk;
                 tkcur[j] = (uint8_t)tk;
+                tiecur[j] = (uint8_t)tie;
                 wt_l += (int64_t)jc(j, s).w * tk;
-                tie_l += jc(j, s).w * (cnt<true>(j, s, rho, lcur[j]) - tk);
+                tie_l += jc(j, s).w * tie;
             });
             const int64_t wt = blk.sum(wt_l);
             wgt_star = wt;
@@ -552,7 +564,7 @@ struct Ctx {
             int64_t used_l = 0;
             for_jobs([&](int j, int s) {
                 const int tk = tkcur[j];
-                const int tie = cnt<true>(j, s, rho, lcur[j]) - tk;
+                const int tie = tiecur[j];
                 const int64_t wj = jc(j, s).w;
                 int tt;
                 if (excl + wj * tie <= rem) tt = tie;
@@ -587,9 +599,13 @@ struct Ctx {
         }
         double fs = 0.0, gm = 0.0, ub = 0.0;
         for_jobs([&](int j, int s) {
-            fs = fs + fval(j, s, ncur[j]);
-            gm = sw_max(gm, gval(j, s, ncur[j]));
-            ub = ub + fval(j, s, lcur[j] + tkcur[j]);
+            /* the bound's count l + taken equals n for every job outside the
+             * tie group and the width tail: one f evaluation serves both */
+            const int nj = ncur[j], lt = lcur[j] + tkcur[j];
+            const double fn = fval(j, s, nj);
+            fs = fs + fn;
+            gm = sw_max(gm, gval(j, s, nj));
+            ub = ub + (lt == nj ? fn : fval(j, s, lt));
         });
         blk.detsum_max(fs, gm, ev.U, ev.Mact);
         ev.J = ev.U - k * ev.Mact;
@@ -619,9 +635,7 @@ struct Ctx {
     __device__ __forceinline__ int64_t levels_between(double a, double b) {
         int64_t c = 0;
         for_jobs([&](int j, int s) {
-            const sw_jobc& cj = jc(j, s);
-            const int n1 = Tj(j, s) + 1;
-            const int d = g_count_gt(cj, n1, a) - g_count_ge(cj, n1, b);
+            const int d = g_cnt<false>(j, s, a) - g_cnt<true>(j, s, b);
             c += d > 0 ? d : 0;
         });
         c = blk.sum(c);
@@ -1373,7 +1387,7 @@ __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
                r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) + r16(sizeof(sw_repair_t));
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
-        s += 7 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK) + SW_JOB_LDS_BYTES;
+        s += 8 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK) + SW_JOB_LDS_BYTES;
     }
     return s;
 }
@@ -1442,6 +1456,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.placed = carve(NJ);
         c.placed2 = carve(NJ);
         c.nfin = carve(NJ);
+        c.tiecur = carve(NJ);
         c.pst = nullptr;
         c.pord = nullptr;
         c.pmask = nullptr;
@@ -1466,6 +1481,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.placed = u8 + 4 * (size_t)N;
         c.placed2 = u8 + 5 * (size_t)N;
         c.nfin = u8 + 6 * (size_t)N;
+        c.tiecur = u8 + 7 * (size_t)N;
         uint64_t* m64 = B.ws.u64 + SW_WS_U64 * jo;
         c.ycur = m64;
         c.ybest = m64 + N;
