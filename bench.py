@@ -109,6 +109,9 @@ def parse():
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
                     help="c3: batched 900x30 instances per GPU (headline, replicas); "
                          "c4: one 10k x 30 instance sharded across the ranks (RCCL)")
+    ap.add_argument("--transport", choices=("rccl", "peer"), default="rccl",
+                    help="--workload c4: step collectives on RCCL, or on the peer-memory transport "
+                         "(sw_dist_enable_peer; at one rank RCCL stays)")
     ap.add_argument("--c4-steps", dest="c4_steps", type=int, default=20,
                     help="sharded C4 solves timed for the c4_sharded sub-record")
     ap.add_argument("--no-c4", dest="no_c4", action="store_true",
@@ -164,6 +167,8 @@ def main_c4(args, world, rank, local, dist):
     if dist is not None:
         dist.broadcast_object_list(uid, src=0)
     solver.dist_init(uid[0], rank, world)
+    if args.transport == "peer":
+        solver.dist_enable_peer(a.N)
 
     def barrier():
         torch.cuda.synchronize()
@@ -216,6 +221,7 @@ def main_c4(args, world, rank, local, dist):
                                    f"k={a.k:g}; jobs split over {world} ranks",
                        "jobs": a.N, "rounds": a.T, "parallelism": f"jobs sharded x{world}"},
             "collective_steps": r["iters"],
+            "transport": args.transport,
             "objective": r["objective"],
             "host_boundary_solves_per_s": hsteps / host_elapsed,
         }
