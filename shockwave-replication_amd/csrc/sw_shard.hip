@@ -29,10 +29,10 @@
  *        K price/level probes per pass (K-ary search)
  *   k_assign   thread per job: the job-ordered tie group, block offsets
  *        from k_take's per-block tie sums plus a block scan
- *   k_eval_jobs / k_eval_lanes   per-job values (thread per job), then one
- *        workgroup sums each deterministic-sum lane left to right (sw_detsum's
+ *   k_eval     per-job values (thread per job) into LDS, then a thread per
+ *        deterministic-sum lane sums its jobs left to right (sw_detsum's
  *        chunks), so the gathered lanes reproduce the single-instance sums
- *        bit for bit
+ *        bit for bit; one launch per reduction step
  *   k_pack_chunk_sort / k_pack_merge_rank   the global placement order: LDS
  *        bitonic sort per 1024-entry chunk, ranks by binary searches in the
  *        other sorted chunks
@@ -474,15 +474,29 @@ __global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
 
 /* ---- reductions with deterministic lane sums ------------------------------- */
 
-/* Per-job values of a reduction step: xa[i] (A row), xa[NL + i] (B row);
- * red[0] = max g (bits), red[1] = integer sum.  SW_EV_FINAL also writes the
- * plan row and count of job i. */
-__global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const int32_t* arr,
-                                                   const uint64_t* ysrc, int arr_a, int arr_b) {
-    const int i = blockIdx.x * kTB + threadIdx.x;
+/* A reduction step in ONE kernel.  Block b owns the deterministic-sum lanes
+ * [b·lpb, (b+1)·lpb) of this rank (lane ℓ sums the jobs [ℓ·q, ℓ·q + q),
+ * sw_detsum's chunks): its threads compute the per-job values of those
+ * lanes' jobs (thread per job) into LDS, then lpb threads sum each lane left
+ * to right — so the gathered lanes reproduce the single-instance sums bit for
+ * bit.  max g and the integer sum go to red[0] / red[1] by atomics; the last
+ * block to finish (counter red[kRedCtr]) copies them behind the lanes.
+ * out = [A lanes][B lanes][gm][isum].  SW_EV_FINAL also writes the plan row
+ * and count of each job. */
+constexpr int kRedCtr = 120; /* a step-result slot no step uses: eval's block counter */
+__global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t* arr,
+                                             const uint64_t* ysrc, int arr_a, int arr_b, int lpb,
+                                             double* out) {
+    __shared__ double xs[2][kTB];
+    __shared__ long long wred[kTB / 64];
+    __shared__ unsigned long long wmax[kTB / 64];
+    __shared__ int last;
+    const int64_t q = S.q;
+    const int64_t lane0 = (int64_t)blockIdx.x * lpb;
+    const int64_t i = lane0 * q + (int64_t)threadIdx.x; /* local job of this thread */
     double fa = 0.0, fb = 0.0, gm = 0.0;
     long long is = 0;
-    if (i < S.NL) {
+    if ((int64_t)threadIdx.x < (int64_t)lpb * q && i < S.NL) {
         const sw_jobc c = S.jc[i];
         if (sel == SW_EV_SELECT) {
             const int n = S.arr[SW_A_N][i];
@@ -518,35 +532,47 @@ __global__ __launch_bounds__(kTB) void k_eval_jobs(ShardDev S, int sel, const in
             gm = sw_g(&c, cn);
             is = cn > 0;
         }
-        S.xa[i] = fa;
-        S.xa[(size_t)S.NL + i] = fb;
     }
-    red_umax(S.red + 0, sw_bits(gm)); /* g ≥ 0: bit order = value order */
-    red_add(S.red + 1, is);
-}
-
-/* Thread ℓ < LW owns deterministic-sum lane rank·LW + ℓ: the left-to-right
- * sum of its jobs [L·q, L·q + q) (sw_detsum), for both rows.
- * Writes [A lanes][B lanes][gm][isum] to out. */
-__global__ __launch_bounds__(SW_BLOCK) void k_eval_lanes(ShardDev S, double* out) {
-    const int lane = threadIdx.x;
-    if (lane < S.LW) {
-        const int64_t L = (int64_t)S.rank * S.LW + lane;
-        const int64_t j0 = L * S.q, j1 = min(S.N, j0 + S.q);
-        double fa = 0.0, fb = 0.0;
-        const double* xa = S.xa - S.off;
-        const double* xb = S.xa + S.NL - S.off;
-#pragma unroll 4
-        for (int64_t j = j0; j < j1; ++j) {
-            fa = fa + xa[j];
-            fb = fb + xb[j];
-        }
-        out[lane] = fa;
-        out[S.LW + lane] = fb;
-    }
+    xs[0][threadIdx.x] = fa;
+    xs[1][threadIdx.x] = fb;
+    /* block max / sum, one atomic each per block */
+    const unsigned long long gb = wave_max((unsigned long long)sw_bits(gm)); /* g ≥ 0: bit order = value order */
+    const long long sb = wave_sum(is);
+    if (lane_id() == 0) { wmax[wave_id()] = gb; wred[wave_id()] = sb; }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        out[2 * S.LW] = sw_from_bits((uint64_t)S.red[0]);
-        reinterpret_cast<long long*>(out)[2 * S.LW + 1] = S.red[1];
+        unsigned long long m = 0;
+        long long t = 0;
+        for (int w = 0; w < kTB / 64; ++w) { m = wmax[w] > m ? wmax[w] : m; t += wred[w]; }
+        if (m) atomicMax((unsigned long long*)(S.red + 0), m);
+        if (t) atomicAdd((unsigned long long*)(S.red + 1), (unsigned long long)t);
+    }
+    /* lane sums, left to right over the lane's jobs present on this rank */
+    const int64_t lane = lane0 + (int64_t)threadIdx.x;
+    if ((int)threadIdx.x < lpb && lane < S.LW) {
+        const int64_t jb = lane * q, je = min((int64_t)S.NL, jb + q);
+        double a = 0.0, b = 0.0;
+        for (int64_t j = jb; j < je; ++j) {
+            a = a + xs[0][j - lane0 * q];
+            b = b + xs[1][j - lane0 * q];
+        }
+        out[lane] = a;
+        out[S.LW + lane] = b;
+    }
+    /* the last block publishes max g and the sum behind the lanes */
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = atomicAdd((unsigned long long*)(S.red + kRedCtr), 1ull) == (unsigned long long)(gridDim.x - 1);
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        const unsigned long long g = __hip_atomic_load((unsigned long long*)(S.red + 0), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t = __hip_atomic_load((unsigned long long*)(S.red + 1), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        out[2 * S.LW] = sw_from_bits(g);
+        reinterpret_cast<long long*>(out)[2 * S.LW + 1] = (long long)t;
     }
 }
 
@@ -1325,9 +1351,11 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     SH_TRY(zero_red(S, 2));
     const int32_t* arr = sel == SW_EV_GMAX || sel == SW_EV_PACKED ? S->arr[arg].p : nullptr;
     const uint64_t* ys = sel == SW_EV_FINAL ? S->y[arg].p : nullptr;
-    LAUNCH(S, k_eval_jobs, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (int)sel, arr, ys,
-           (int)(arg & 0xFF), (int)(arg >> 8));
-    LAUNCH(S, k_eval_lanes, dim3(1), dim3(SW_BLOCK), 0, S->h->stream, S->dv, S->xsend.p);
+    /* lanes per block: a block's jobs (lpb lanes × q) fit its kTB threads */
+    const int lpb = (int)std::max<int64_t>(1, kTB / S->q);
+    if (S->q > kTB) return S->h->err = "eval: more than 256 jobs per lane", SW_ERR_CAPACITY;
+    LAUNCH(S, k_eval, dim3((unsigned)((LW + lpb - 1) / lpb)), dim3(kTB), 0, S->h->stream, S->dv,
+           (int)sel, arr, ys, (int)(arg & 0xFF), (int)(arg >> 8), lpb, S->xsend.p);
     std::vector<double> all((size_t)blk * S->world);
     SH_TRY(coll_gather(S, S->xsend.p, S->xrecv.p, (size_t)blk * 8, all.data()));
     double g = 0.0;
