@@ -94,8 +94,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16384,
-                    help="instances per GPU per step (64 per CU: one 512-thread workgroup fits a "
+    ap.add_argument("--batch", type=int, default=32768,
+                    help="instances per GPU per step (128 per CU: one 512-thread workgroup fits a "
                          "CU at a time, and a launch ends with its most expensive instances "
                          "running on a few CUs, so more instances per launch amortise that tail: "
                          "1.198M / 1.237M / 1.286M / 1.301M plan-solves/s at 4096 / 8192 / 16384 / "

@@ -851,7 +851,9 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
             for (int p = 0; p < W; ++p) reinterpret_cast<unsigned long long*>(ps.base[p] + off)[i] = v;
         }
     }
-    __threadfence_system();
+    /* the workgroup barrier orders every thread's payload stores before the
+     * flag writers' system-scope releases (release cumulativity), so one
+     * release per flag publishes the whole payload */
     __syncthreads();
     if ((int)threadIdx.x < W)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(ps.base[threadIdx.x]) + rank, seq,
@@ -899,7 +901,6 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
         if (!bad)
             for (int i = threadIdx.x; i < words; i += 256) hdst[i] = from[i];
         if (threadIdx.x == 0) hdst[words] = bad ? 1u : 0u;
-        __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_store(hflag, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }

@@ -9,7 +9,7 @@ TAG=${1:-final_r2d}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B=16384
+B=32768
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err &&
