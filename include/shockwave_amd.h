@@ -244,8 +244,10 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
  * communicator set up by the init call is used once, to exchange the region
  * handles.  max_total_jobs bounds the instances (total_jobs) later solves
  * may pass (the regions are sized from it; larger ones return
- * SW_ERR_CAPACITY).  World 1 keeps the init call's transport.  Results are
- * the same bits as with RCCL or host collectives.
+ * SW_ERR_CAPACITY).  World 1 keeps the init call's transport.  If any rank
+ * cannot allocate or map its side, every rank returns an error and keeps
+ * the init call's transport.  Results are the same bits as with RCCL or host
+ * collectives.
  */
 #define SW_PEER_MAX_WORLD 64
 int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs);

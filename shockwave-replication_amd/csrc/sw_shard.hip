@@ -1659,61 +1659,94 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
     if (W > SW_PEER_MAX_WORLD) return h->err = "peer transport: world exceeds SW_PEER_MAX_WORLD", SW_ERR_INVALID;
     if (S->peer) return h->err = "peer transport already enabled", SW_ERR_INVALID;
     if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
+    if (!S->host_comm && !S->comm)
+        return h->err = "peer transport: sw_dist_init or sw_dist_init_host first", SW_ERR_INVALID;
+    /* an all-gather on the init call's collective (setup only) */
+    auto gather = [&](const void* send, void* recv, size_t n) -> int {
+        if (S->host_comm)
+            return S->hc.allgather(S->hc.ctx, send, recv, (int64_t)n) ? host_fail(S, "peer setup all-gather")
+                                                                       : SW_OK;
+        DevBuf<unsigned char> ds, dr;
+        if (ds.reserve(n) || dr.reserve(n * (size_t)W)) return h->err = "peer setup: allocation", SW_ERR_HIP;
+        SH_HIP(S, hipMemcpy(ds.p, send, n, hipMemcpyHostToDevice));
+        SH_NCCL(S, ncclAllGather(ds.p, dr.p, n, ncclUint8, S->comm, h->stream));
+        SH_HIP(S, hipStreamSynchronize(h->stream));
+        SH_HIP(S, hipMemcpy(recv, dr.p, n * (size_t)W, hipMemcpyDeviceToHost));
+        return SW_OK;
+    };
+    auto undo = [&]() {
+        for (int p = 0; p < SW_PEER_MAX_WORLD; ++p)
+            if (S->opened[p]) { (void)hipIpcCloseMemHandle(S->opened[p]); S->opened[p] = nullptr; }
+        if (S->xreg) (void)hipFree(S->xreg);
+        if (S->xerr) (void)hipFree(S->xerr);
+        S->xreg = nullptr;
+        S->xerr = nullptr;
+    };
     const long long slot = peer_slot_bytes(max_total_jobs, W);
     const long long half = slot * W;
     const size_t bytes = (size_t)kXHdr + 2 * (size_t)half;
-    /* fine-grained device memory: peers write it over xGMI, and this GPU's
-     * L2 must not hold stale copies of those lines */
-    void* reg = nullptr;
-    if (hipExtMallocWithFlags(&reg, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-        (void)hipGetLastError();
-        SH_HIP(S, hipMalloc(&reg, bytes));
-    }
-    S->xreg = (unsigned char*)reg;
-    SH_HIP(S, hipMemset(S->xreg, 0, bytes));
-    SH_HIP(S, hipMalloc((void**)&S->xerr, sizeof(int)));
-    SH_HIP(S, hipMemset(S->xerr, 0, sizeof(int)));
-    SH_HIP(S, hipDeviceSynchronize());
-    /* every rank: {pid, region pointer, IPC handle}, all-gathered on the init
-     * call's collective */
+    /* every rank: {ok, pid, region pointer, IPC handle}.  A local failure is
+     * carried through both all-gathers instead of returning early, so that
+     * every rank reaches them and all ranks keep the init call's transport
+     * together when any rank could not set up its side. */
     struct Rec {
-        long long pid;
+        long long ok, pid;
         unsigned long long ptr;
         hipIpcMemHandle_t ih;
     };
     Rec mine;
     memset(&mine, 0, sizeof(mine));
     mine.pid = (long long)getpid();
-    mine.ptr = (unsigned long long)(uintptr_t)S->xreg;
-    SH_HIP(S, hipIpcGetMemHandle(&mine.ih, S->xreg));
-    std::vector<Rec> all((size_t)W);
-    if (S->host_comm) {
-        if (S->hc.allgather(S->hc.ctx, &mine, all.data(), (int64_t)sizeof(Rec)))
-            return host_fail(S, "peer handle all-gather");
-    } else if (S->comm) {
-        DevBuf<unsigned char> dsend, drecv;
-        if (dsend.reserve(sizeof(Rec)) || drecv.reserve(sizeof(Rec) * (size_t)W))
-            return h->err = "peer transport: allocation failed", SW_ERR_HIP;
-        SH_HIP(S, hipMemcpy(dsend.p, &mine, sizeof(Rec), hipMemcpyHostToDevice));
-        SH_NCCL(S, ncclAllGather(dsend.p, drecv.p, sizeof(Rec), ncclUint8, S->comm, h->stream));
-        SH_HIP(S, hipStreamSynchronize(h->stream));
-        SH_HIP(S, hipMemcpy(all.data(), drecv.p, sizeof(Rec) * (size_t)W, hipMemcpyDeviceToHost));
-        dsend.release();
-        drecv.release();
-    } else {
-        return h->err = "peer transport: sw_dist_init or sw_dist_init_host first", SW_ERR_INVALID;
+    {
+        /* fine-grained device memory: peers write it over xGMI, and this
+         * GPU's L2 must not hold stale copies of those lines */
+        void* reg = nullptr;
+        if (hipExtMallocWithFlags(&reg, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            if (hipMalloc(&reg, bytes) != hipSuccess) reg = nullptr;
+        }
+        S->xreg = (unsigned char*)reg;
+        bool ok = reg != nullptr && hipMemset(reg, 0, bytes) == hipSuccess &&
+                  hipMalloc((void**)&S->xerr, sizeof(int)) == hipSuccess &&
+                  hipMemset(S->xerr, 0, sizeof(int)) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+                  hipIpcGetMemHandle(&mine.ih, reg) == hipSuccess;
+        mine.ok = ok ? 1 : 0;
+        mine.ptr = (unsigned long long)(uintptr_t)reg;
+        (void)hipGetLastError();
     }
-    for (int32_t p = 0; p < W; ++p) {
+    std::vector<Rec> all((size_t)W);
+    {
+        const int rc = gather(&mine, all.data(), sizeof(Rec));
+        if (rc < 0) { undo(); return rc; }
+    }
+    long long ok = 1;
+    for (int32_t p = 0; p < W; ++p) ok &= all[(size_t)p].ok;
+    for (int32_t p = 0; p < W && ok; ++p) {
         if (p == S->rank) {
             S->ps.base[p] = S->xreg;
         } else if (all[(size_t)p].pid == mine.pid) { /* same process: the pointer itself */
             S->ps.base[p] = (unsigned char*)(uintptr_t)all[(size_t)p].ptr;
         } else {
             void* q = nullptr;
-            SH_HIP(S, hipIpcOpenMemHandle(&q, all[(size_t)p].ih, hipIpcMemLazyEnablePeerAccess));
+            if (hipIpcOpenMemHandle(&q, all[(size_t)p].ih, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();
+                ok = 0;
+                break;
+            }
             S->opened[p] = q;
             S->ps.base[p] = (unsigned char*)q;
         }
+    }
+    std::vector<long long> oks((size_t)W);
+    {
+        const int rc = gather(&ok, oks.data(), sizeof(long long));
+        if (rc < 0) { undo(); return rc; }
+    }
+    for (int32_t p = 0; p < W; ++p) ok &= oks[(size_t)p];
+    if (!ok) {
+        undo();
+        return h->err = "peer transport: a rank could not map the exchange regions (init transport kept)",
+               SW_ERR_HIP;
     }
     S->xslot = slot;
     S->xhalf = half;
