@@ -425,6 +425,17 @@ def c5_share(probs, world, rank):
     return [p for i, p in enumerate(probs) if (i // ng) % world == rank]
 
 
+def c5_order(probs):
+    """Launch order of a rank's sweep instances: longest first.  Workgroups
+    start in instance order and the sweep ends when its last CU does, so the
+    expensive instances go first and the cheap ones fill the CUs that free up
+    (longest-processing-time-first list scheduling).  The cost key is the
+    configuration's: the small-k level search (k = 1e-3, ~210 passes) before
+    k = 10 (~31-38) before k = 1e5 (~24), DESIGN.md §7.1.  Results are per
+    instance, so the order changes no result."""
+    return sorted(probs, key=lambda a: (a.k, -a.G))
+
+
 def c5_leg(args, world, rank, local, dist):
     """The C5 sub-record (BASELINE configs[4]): a FIXED sweep
     of 512 independent 900-job × 30-round instances, seeds × cluster sizes
@@ -439,7 +450,7 @@ def c5_leg(args, world, rank, local, dist):
     import torch
 
     probs = ss.sweep_problems(C5_INSTANCES, args.jobs, seed0=C5_SEED0, T_override=args.rounds)
-    mine = c5_share(probs, world, rank)
+    mine = c5_order(c5_share(probs, world, rank))
     solver = sn.Solver(device=local)
     solver.upload(mine)
 

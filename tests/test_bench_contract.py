@@ -34,3 +34,11 @@ def test_c5_share_same_mix_every_rank(world):
         mix = collections.Counter(sizes[i % 4] for i in mine)
         assert mix == {G: bench.C5_INSTANCES // 4 // world for G in sizes}, (world, rank, mix)
     assert sorted(seen) == idx
+
+
+def test_c5_order_puts_small_k_first_and_keeps_every_instance():
+    probs = bench.c5_share(ss.sweep_problems(64, N=12), 2, 1)
+    ordered = bench.c5_order(probs)
+    assert sorted(id(p) for p in ordered) == sorted(id(p) for p in probs)
+    ks = [p.k for p in ordered]
+    assert ks == sorted(ks) and ks[0] == 1e-3
