@@ -431,7 +431,9 @@ def c5_order(probs):
     expensive instances go first and the cheap ones fill the CUs that free up
     (longest-processing-time-first list scheduling).  The cost key is the
     configuration's: the small-k level search (k = 1e-3, ~210 passes) before
-    k = 10 (~31-38) before k = 1e5 (~24), DESIGN.md §7.1.  Results are per
+    k = 10 (~31-38) before k = 1e5 (~24), DESIGN.md §7.1 (0.91 ms per sweep
+    on one MI355X, against 1.37 ms in sweep order and 1.00 ms with k = 1e5
+    second).  Results are per
     instance, so the order changes no result."""
     return sorted(probs, key=lambda a: (a.k, -a.G))
 
