@@ -177,7 +177,7 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS || maxT > 32) {
         const int KT = maxT <= 32 ? 32 : 64;
-        if (h->d_ws_u8.reserve(Jz * SW_WS_U8) || h->d_ws_u64.reserve(Jz * SW_WS_U64) ||
+        if (h->d_ws_u8.reserve(Jz * SW_WS_U8) || h->d_ws_u64.reserve(Jz * SW_WS_U64 + (size_t)SW_WS_PAD_U64 * std::max(count, 1)) ||
             h->d_ws_sort.reserve(Jz * 4) || h->d_ws_keys.reserve(Jz * KT) ||
             h->d_ws_jc.reserve(Jz))
             return fail(h, SW_ERR_HIP, "workspace allocation failed");

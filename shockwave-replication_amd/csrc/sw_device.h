@@ -44,6 +44,10 @@ struct sw_ws_dev {
 };
 #define SW_WS_U8 8   /* per-job u8 state arrays   */
 #define SW_WS_U64 6  /* per-job u64 arrays        */
+/* per-instance u64 padding of the u64 workspace: the round loop's position
+ * slots (pmask, pst, pord; slot = (p mod PPL)·64 + p div PPL with
+ * PPL = ⌈A/64⌉) reach up to A + 62, so each slot array holds N + 64 entries */
+#define SW_WS_PAD_U64 192
 
 struct sw_batch_dev {
     const sw_inst_dev* inst;

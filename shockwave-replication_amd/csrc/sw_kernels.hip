@@ -1482,13 +1482,17 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.placed2 = u8 + 5 * (size_t)N;
         c.nfin = u8 + 6 * (size_t)N;
         c.tiecur = u8 + 7 * (size_t)N;
-        uint64_t* m64 = B.ws.u64 + SW_WS_U64 * jo;
+        /* 6N + 192 u64 per instance: three job-indexed rows, then the
+         * three position-slot arrays of N + 64 entries each (pst and pord
+         * use the low half of theirs) */
+        uint64_t* m64 = B.ws.u64 + SW_WS_U64 * jo + (int64_t)SW_WS_PAD_U64 * inst_;
+        const size_t NS = (size_t)N + 64;
         c.ycur = m64;
         c.ybest = m64 + N;
         c.y2 = m64 + 2 * (size_t)N;
         c.pmask = m64 + 3 * (size_t)N;
-        c.pst = (uint32_t*)(m64 + 4 * (size_t)N);
-        c.pord = (int32_t*)(m64 + 5 * (size_t)N);
+        c.pst = (uint32_t*)(m64 + 3 * (size_t)N + NS);
+        c.pord = (int32_t*)(m64 + 3 * (size_t)N + 2 * NS);
         c.sbuf = B.ws.sort + 4 * jo;
         c.gkeys = B.ws.keys + (size_t)KT * jo;
         c.gjc = B.ws.jc + jo;

@@ -1,0 +1,32 @@
+"""Randomised GPU ↔ twin parity (tests/fuzzcases.py): 4,096 instances that
+cover the validator's whole accepted range, solved as heterogeneous batches of
+512 (mixed T, G, k, base grids and widths in one launch), plus 48 instances
+above 1,024 jobs on the HBM-workspace path.  Every field of every result must
+be bit-identical with oracle/plan_twin.c, and every plan must be a valid
+schedule."""
+import pytest
+
+from fuzzcases import fuzz_problem
+from helpers import assert_same_result, check_plan_valid
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 512
+
+
+@pytest.mark.parametrize("chunk", range(8))
+def test_gpu_fuzz_batches_match_twin(chunk, gpu_solver, twin):
+    probs = [fuzz_problem(s) for s in range(chunk * CHUNK, (chunk + 1) * CHUNK)]
+    rb = gpu_solver.solve_batch(probs)
+    for i, (a, r) in enumerate(zip(probs, rb)):
+        what = f"seed {chunk * CHUNK + i} N={a.N} G={a.G} T={a.T} k={a.k:g}"
+        check_plan_valid(a, r)
+        assert_same_result(r, twin.solve(a), what)
+
+
+def test_gpu_fuzz_workspace_path_matches_twin(gpu_solver, twin):
+    probs = [fuzz_problem(100_000 + s, max_n=3000, min_n=1025) for s in range(48)]
+    rb = gpu_solver.solve_batch(probs)
+    for i, (a, r) in enumerate(zip(probs, rb)):
+        check_plan_valid(a, r)
+        assert_same_result(r, twin.solve(a), f"seed {100_000 + i} N={a.N} G={a.G} T={a.T}")
