@@ -170,3 +170,23 @@ def test_gpu_shard_peer_transport_two_processes(tmp_path, twin):
         rs = assemble(a, parts)
         check_plan_valid(a, rs)
         assert_same_as_single(rs, twin.solve(a), f"peer W=2 {case}")
+
+
+def test_gpu_shard_fuzz_rccl_world1(rccl_solver, twin):
+    """The sharded engine over 256 fuzz instances (tests/fuzzcases.py)."""
+    from fuzzcases import fuzz_problem
+
+    for s in range(256):
+        a = fuzz_problem(s)
+        r = rccl_solver.dist_solve(a, 0, a.N)
+        check_plan_valid(a, r)
+        assert_same_as_single(r, twin.solve(a), f"rccl W=1 fuzz seed {s}")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_shard_fuzz_host_comm(world, twin):
+    from fuzzcases import fuzz_problem
+
+    for s in range(256, 256 + 48):
+        a = fuzz_problem(s)
+        assert_same_as_single(gpu_shard_threads(a, world), twin.solve(a), f"W={world} fuzz seed {s}")

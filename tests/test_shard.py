@@ -222,3 +222,16 @@ def test_sharded_gloo_world2(tmp_path, twin):
             parts.append((int(z["lo"]), int(z["hi"]), res))
         rs = assemble(a, parts)
         assert_same_as_single(rs, twin.solve(a), f"gloo case {case}")
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_fuzz_equals_single(world, shard_lib, twin):
+    """The fuzz instances of tests/fuzzcases.py (validator-range inputs, exact
+    duplicate jobs, finished jobs, zero priorities, custom base grids)."""
+    from fuzzcases import fuzz_problem
+
+    for s in range(0, 48):
+        a = fuzz_problem(s)
+        rs = run_threads(shard_lib, a, world)
+        check_plan_valid(a, rs)
+        assert_same_as_single(rs, twin.solve(a), f"W={world} fuzz seed {s}")
