@@ -20,8 +20,10 @@ def _bases(rng):
     return tuple([0.0] + [float(x) for x in inner] + [1.0])
 
 
-def fuzz_problem(seed: int, max_n: int = 1024, min_n: int = 1, off=()) -> sn.ProblemArrays:
-    """off: features to leave out ("done", "smalld", "r0", "p0", "dup", "bases"), with
+def fuzz_problem(seed: int, max_n: int = 1024, min_n: int = 1, off=(),
+                 trace_widths: bool = False) -> sn.ProblemArrays:
+    """trace_widths: widths from {1, 2, 4, 8} only (the reference traces).
+    off: features to leave out ("done", "smalld", "r0", "p0", "dup", "bases"), with
     the same random draws, for narrowing down a mismatch."""
     rng = np.random.default_rng(10_000_019 + seed)
     N = int(np.exp(rng.uniform(np.log(min_n), np.log(max_n + 1)))) if rng.random() < 0.95 else int(
@@ -35,6 +37,8 @@ def fuzz_problem(seed: int, max_n: int = 1024, min_n: int = 1, off=()) -> sn.Pro
     delta = float(rng.choice([120.0, rng.uniform(10.0, 900.0)]))
 
     mode = rng.random()
+    if trace_widths:  # the reference traces' scale factors only
+        mode = 0.0
     if mode < 0.6:
         pw = rng.dirichlet(np.ones(4))
         w = rng.choice(np.array([1, 2, 4, 8]), size=N, p=pw)
