@@ -560,6 +560,46 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
     return ubound_inf - P->k * M_lo;
 }
 
+/* Fill of stranded capacity (the reference MILP packs per
+ * round, shockwave.py:64-75, so its optimum never leaves a round's room to a
+ * job that gains from it).  After the reduced-budget re-solve the best P1 plan
+ * y / n can leave GPUs idle in some rounds: add single rounds there, each time
+ * the candidate (job j with n_j < T_j, first round t without j whose free
+ * capacity fits w_j) of largest gain f(n_j + 1) − f(n_j) (sw_fill_key), until
+ * none has a positive gain or SW_FILL_MAX rounds were added.  The makespan
+ * term can only fall.  Returns the number of rounds added. */
+static int fill_stranded(twin_t* P, int32_t* n, uint8_t* y) {
+    const int32_t N = P->N, T = P->T, G = P->G;
+    int64_t load[SW_TMAX];
+    for (int32_t t = 0; t < T; ++t) load[t] = 0;
+    for (int32_t j = 0; j < N; ++j)
+        for (int32_t t = 0; t < T; ++t)
+            if (y[(size_t)j * T + t]) load[t] += P->jc[j].w;
+    int added = 0;
+    for (int step = 0; step < SW_FILL_MAX; ++step) {
+        uint64_t best = 0;
+        for (int32_t j = 0; j < N; ++j) {
+            if (n[j] >= P->Tj[j]) continue;
+            const int64_t w = P->jc[j].w;
+            int32_t tf = -1;
+            for (int32_t t = 0; t < T; ++t)
+                if (!y[(size_t)j * T + t] && w <= G - load[t]) { tf = t; break; }
+            if (tf < 0) continue;
+            const uint64_t key = sw_fill_key(fval(P, j, n[j] + 1) - fval(P, j, n[j]), j, tf);
+            best = key > best ? key : best;
+        }
+        P->passes++;
+        if (best == 0) break;
+        const int64_t jb = sw_fill_job(best);
+        const int32_t tb = sw_fill_round(best);
+        y[(size_t)jb * T + tb] = 1;
+        n[jb] += 1;
+        load[tb] += P->jc[jb].w;
+        ++added;
+    }
+    return added;
+}
+
 /* Full plan solve; same contract as sw_plan_solve in include/shockwave_amd.h. */
 int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     if (sw_validate_problem(pr) != 0) return SW_ERR_INVALID;
@@ -668,6 +708,13 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         if (deficit == 0) break;
         status |= SW_STATUS_P1_REPACKED;
         P.C -= deficit;
+    }
+    /* a re-solved P1 can strand capacity: fill it (the filled plan is no
+     * longer a density pack, so P2 starts from (a) again) */
+    if ((status & SW_STATUS_P1_REPACKED) && fill_stranded(&P, nbest, ybest) > 0) {
+        dens_best = 0;
+        rep_best = 0;
+        dskip_best = 0;
     }
     memcpy(nb, nbest, sizeof(int32_t) * NN);
     memcpy(y1, ybest, NN * (size_t)T); /* y1 = best P1 plan */

@@ -231,6 +231,34 @@ static int e_tail_apply(void* ctx, int64_t jb) {
     return 0;
 }
 
+static int e_fill_best(void* ctx, const int64_t* load, uint64_t* best) {
+    eng_t* E = (eng_t*)ctx;
+    uint64_t b = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int32_t n = E->arr[SW_A_NFIN][i];
+        if (n >= E->Tj[i]) continue;
+        const uint64_t m = E->y[SW_Y_BEST][i];
+        const int64_t w = E->jc[i].w;
+        int32_t tf = -1;
+        for (int32_t t = 0; t < E->T; ++t)
+            if (!((m >> t) & 1u) && w <= E->G - load[t]) { tf = t; break; }
+        if (tf < 0) continue;
+        const uint64_t kk = sw_fill_key(fv(E, i, n + 1) - fv(E, i, n), E->off + i, tf);
+        b = kk > b ? kk : b;
+    }
+    *best = b;
+    return E->comm->allreduce_max_u64(E->comm->ctx, best, 1);
+}
+
+static int e_fill_apply(void* ctx, int64_t jb, int32_t t) {
+    eng_t* E = (eng_t*)ctx;
+    if (jb >= E->off && jb < E->off + E->NL) {
+        E->y[SW_Y_BEST][jb - E->off] |= (uint64_t)1 << t;
+        E->arr[SW_A_NFIN][jb - E->off] += 1;
+    }
+    return 0;
+}
+
 static int e_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
                   int64_t* isum) {
     eng_t* E = (eng_t*)ctx;
@@ -463,6 +491,8 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.pack = e_pack;
     ops.class_caps = e_class_caps;
     ops.pack_class = e_pack_class;
+    ops.fill_best = e_fill_best;
+    ops.fill_apply = e_fill_apply;
     ops.search = NULL; /* the controller's own K-ary loop */
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,

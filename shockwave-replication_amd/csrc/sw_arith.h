@@ -145,6 +145,24 @@ SW_HD double sw_pos(double v) { return v > 0.0 ? v : 0.0; }
  * Ratios that agree to 2^-41 are ordered by job index, like exact ties. */
 SW_HD uint64_t sw_ratio_key(double r) { return sw_bits(r) >> 11; }
 
+/* Fill of stranded capacity: when P1 needed the reduced-
+ * budget re-solve, single rounds are added into rounds with room, largest
+ * utility gain f(n+1) − f(n) first.  Key of one candidate: the gain in fp32
+ * (clamped to [FLT_MIN, FLT_MAX], so every positive gain keeps a nonzero
+ * key), then the job index descending (26 bits), then the round (6 bits);
+ * 0 when the gain is not positive.  At most SW_FILL_MAX rounds are added. */
+#define SW_FILL_MAX 512
+SW_HD uint64_t sw_fill_key(double gain, int64_t j, int32_t t) {
+    if (!(gain > 0.0)) return 0;
+    double k = gain;
+    if (k < SW_FLT_MIN) k = SW_FLT_MIN;
+    if (k > SW_FLT_MAX) k = SW_FLT_MAX;
+    const uint32_t gb = sw_fbits_of((float)k);
+    return ((uint64_t)gb << 32) | ((uint64_t)(0x3FFFFFFu - (uint32_t)j) << 6) | (uint64_t)t;
+}
+SW_HD int64_t sw_fill_job(uint64_t key) { return (int64_t)(0x3FFFFFFu - (uint32_t)((key >> 6) & 0x3FFFFFFu)); }
+SW_HD int32_t sw_fill_round(uint64_t key) { return (int32_t)(key & 63u); }
+
 /* Golden-section constants (fp64 literals, identical on both sides). */
 #define SW_GS_A 0.3819660112501051
 #define SW_GS_B 0.6180339887498949

@@ -1603,6 +1603,54 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         }
         __syncthreads();
     }
+    /* ---- fill of stranded capacity (twin: fill_stranded): a re-solved P1
+     *      can leave round capacity idle; add single rounds there, largest
+     *      utility gain first (sw_fill_key), one block max per round ---- */
+    if (status & SW_STATUS_P1_REPACKED) {
+        int32_t* load = c.caps; /* spare pack row, free until class-wise P2 */
+        if (threadIdx.x < 64) load[threadIdx.x] = 0;
+        __syncthreads();
+        c.for_jobs([&](int j, int s) {
+            const uint64_t m = c.ybest[j];
+            const int32_t w = c.jc(j, s).w;
+            for (int t = 0; t < c.T; ++t)
+                if ((m >> t) & 1ull) atomicAdd(&load[t], w);
+        });
+        __syncthreads();
+        int added = 0;
+        for (int step = 0; step < SW_FILL_MAX; ++step) {
+            uint64_t best = 0;
+            c.for_jobs([&](int j, int s) {
+                const int n = c.nfin[j];
+                if (n >= c.Tj(j, s)) return;
+                const uint64_t m = c.ybest[j];
+                const int32_t w = c.jc(j, s).w;
+                int tf = -1;
+                for (int t = 0; t < c.T; ++t)
+                    if (!((m >> t) & 1ull) && w <= c.G - load[t]) { tf = t; break; }
+                if (tf < 0) return;
+                const uint64_t key = sw_fill_key(c.fval(j, s, n + 1) - c.fval(j, s, n), j, tf);
+                best = key > best ? key : best;
+            });
+            best = c.blk.umax(best); /* its barrier: every thread has read load */
+            c.passes++;
+            if (best == 0) break;
+            const int jb = (int)sw_fill_job(best);
+            const int tb = sw_fill_round(best);
+            if (jb >= c.jlo() && jb < c.jhi()) {
+                c.ybest[jb] |= 1ull << tb;
+                c.nfin[jb] = (uint8_t)(c.nfin[jb] + 1);
+            }
+            if (threadIdx.x == 0) load[tb] += c.w_in[jb];
+            ++added;
+            __syncthreads();
+        }
+        if (added > 0) {
+            dens_best = false;
+            rep_best = false;
+            dskip_best = false;
+        }
+    }
     /* ---- P2 (twin: the P2 block): (a) density order, (b) weight order,
      *      (c) class-wise inside the P1 profile — first that places every
      *      round, else the P1 placement ---- */

@@ -472,6 +472,36 @@ __global__ __launch_bounds__(kTB) void k_tail_best(ShardDev S, long long rem2) {
 
 __global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
 
+/* fill of stranded capacity (sw_shard_ops.fill_best / fill_apply) */
+struct FillLoad {
+    long long v[SW_TMAX]; /* GPUs in use per round, all ranks */
+};
+
+__global__ __launch_bounds__(kTB) void k_fill_best(ShardDev S, FillLoad L) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t best = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int n = S.arr[SW_A_NFIN][i];
+        if (n < tj_of(S, c)) {
+            const uint64_t m = S.y[SW_Y_BEST][i];
+            int tf = -1;
+            for (int t = 0; t < S.T; ++t)
+                if (!((m >> t) & 1ull) && (long long)c.w <= (long long)S.G - L.v[t]) { tf = t; break; }
+            if (tf >= 0)
+                best = sw_fill_key(sw_f(&c, n + 1, S.nb, S.beta, S.ell, S.slope) -
+                                       sw_f(&c, n, S.nb, S.beta, S.ell, S.slope),
+                                   S.off + i, tf);
+        }
+    }
+    red_umax(S.red + 0, best);
+}
+
+__global__ void k_fill_apply(ShardDev S, int i, int t) {
+    S.y[SW_Y_BEST][i] |= 1ull << t;
+    S.arr[SW_A_NFIN][i] += 1;
+}
+
 /* ---- reductions with deterministic lane sums ------------------------------- */
 
 /* A reduction step in ONE kernel.  Block b owns the deterministic-sum lanes
@@ -1345,6 +1375,22 @@ int op_tail_apply(void* ctx, int64_t jb) {
     return SW_OK;
 }
 
+int op_fill_best(void* ctx, const int64_t* load, uint64_t* best) {
+    auto* S = (sw_shard_state*)ctx;
+    FillLoad L;
+    for (int t = 0; t < SW_TMAX; ++t) L.v[t] = t < S->dv.T ? (long long)load[t] : 0;
+    SH_TRY(zero_red(S, 1));
+    LAUNCH(S, k_fill_best, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, L);
+    return coll_reduce(S, S->dv.red, 1, 1, best);
+}
+
+int op_fill_apply(void* ctx, int64_t jb, int32_t t) {
+    auto* S = (sw_shard_state*)ctx;
+    if (jb >= S->off && jb < S->off + S->NL)
+        LAUNCH(S, k_fill_apply, dim3(1), dim3(1), 0, S->h->stream, S->dv, (int)(jb - S->off), (int)t);
+    return SW_OK;
+}
+
 int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
             int64_t* isum) {
     auto* S = (sw_shard_state*)ctx;
@@ -1793,6 +1839,8 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.assign = op_assign;
     ops.tail_best = op_tail_best;
     ops.tail_apply = op_tail_apply;
+    ops.fill_best = op_fill_best;
+    ops.fill_apply = op_fill_apply;
     ops.eval = op_eval;
     ops.copy = op_copy;
     ops.copy_y = op_copy_y;

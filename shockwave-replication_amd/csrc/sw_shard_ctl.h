@@ -117,6 +117,13 @@ typedef struct sw_shard_ops {
      * and leaves every other job untouched */
     int (*pack_class)(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
                       int32_t pdst);
+    /* fill of stranded capacity (twin: fill_stranded): best = max over jobs
+     * with arr[SW_A_NFIN]_j < T_j of sw_fill_key(f(n+1) − f(n), j, t), t the
+     * first round without j in Y[SW_Y_BEST] with w_j ≤ G − load[t] (0 if
+     * none); fill_apply sets bit t of job jb's Y[SW_Y_BEST] row and adds one
+     * to its arr[SW_A_NFIN] on the owning rank */
+    int (*fill_best)(void* ctx, const int64_t* load, uint64_t* best);
+    int (*fill_apply)(void* ctx, int64_t jb, int32_t t);
     /* optional (NULL = the controller drives count_gt / feasible itself):
      * the whole K-ary search of swc_search inside the engine — kind 0 over
      * count_gt, 1 over feasible — returning its answer and the number of
@@ -490,6 +497,40 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             if (deficit == 0) break;
             status |= SW_STATUS_P1_REPACKED;
             c->C -= deficit;
+        }
+        /* a re-solved P1 can strand capacity: fill it (twin: fill_stranded);
+         * the per-round load comes from the width classes' round counts */
+        if (status & SW_STATUS_P1_REPACKED) {
+            int64_t load[SW_TMAX];
+            int32_t caps[SW_TMAX];
+            int32_t next_w = 0;
+            int64_t md[2];
+            for (int32_t t = 0; t < T; ++t) load[t] = 0;
+            SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, 0, -1, caps, &next_w, md));
+            c->steps++;
+            while (next_w != 0x7FFFFFFF) {
+                const int32_t wc = next_w;
+                SWC_RUN(o->class_caps(o->ctx, SW_A_NFIN, SW_Y_BEST, wc, -1, caps, &next_w, md));
+                c->steps++;
+                for (int32_t t = 0; t < T; ++t) load[t] += (int64_t)wc * caps[t];
+            }
+            int added = 0;
+            for (int step = 0; step < SW_FILL_MAX; ++step) {
+                uint64_t best;
+                SWC_RUN(o->fill_best(o->ctx, load, &best));
+                c->steps++;
+                if (best == 0) break;
+                const int64_t jb = sw_fill_job(best);
+                const int32_t tb = sw_fill_round(best);
+                SWC_RUN(o->fill_apply(o->ctx, jb, tb));
+                load[tb] += c->w_all[jb];
+                ++added;
+            }
+            if (added > 0) {
+                dens_best = 0;
+                rep_best = 0;
+                dskip_best = 0;
+            }
         }
         /* P2: priority placement of the best packed counts (shockwave.py:281-328);
          * (a) density order, (b) weight order, (c) class-wise inside the P1

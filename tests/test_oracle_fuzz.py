@@ -7,8 +7,8 @@ every instance must be within the north star's 1e-3 of the MILP optimum: 307
 instances (N ≤ 60, T ≤ 12, any k, λ, base grid, duplicates, finished jobs).
 Below it, width fragmentation is the recorded exception:
 measured over the first 1,300 seeds at N ≤ 80, T ≤ 12, 1 of 1,057 instances
-with G ≥ 2·max width exceeded 1e-3 (G = 22: 7.1e-3; G = 10: 2.4e-3), and 10
-of 175 with G < 2·max width (worst 0.37)."""
+with G ≥ 2·max width exceeds 1e-3 (G = 22: 2.8e-3), and 4 of 175 with
+G < 2·max width (worst 6.8e-2)."""
 import pytest
 
 import milp_ref as mr

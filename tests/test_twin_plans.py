@@ -4,7 +4,8 @@ tests/golden/twin_plans.json holds, for 32 seeded instances at the reference
 cluster configurations (scale_{32,64,128,256}gpus.json's k and lambda), the
 objective bits and MD5 digests of the plan and counts of the CPU twin
 (generator: tests/golden/make_twin_plans.py; re-pinned when the P2 cascade
-gained the width-profile repair).  Performance-only changes of the kernel or
+gained the width-profile repair, and when P1 gained the fill of stranded
+capacity, which changed case 25, a re-solved one, to a higher objective).  Performance-only changes of the kernel or
 the searches must keep them: the twin and the GPU kernel must both reproduce
 every digest.
 """
