@@ -70,3 +70,45 @@ def test_gpu_mmf_rejects_bad_input(gpu_solver):
         gpu_solver.mmf_allocate([1, 0], [1.0, 1.0], 4)
     with pytest.raises(sn.NativeError):
         gpu_solver.mmf_allocate([1, 1], [1.0, -1.0], 4)
+
+
+def fuzz_instances(n_cases, seed=11, max_n=5000):
+    """Random MaxMinFairness inputs: sizes 1..max_n (log-uniform), clusters of
+    1..2048 GPUs, scale factors from the traces or up to 255, coefficients over
+    six decades, exact duplicates."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_cases):
+        n = int(np.exp(rng.uniform(0.0, np.log(max_n + 1))))
+        n = max(1, min(n, max_n))
+        G = int(np.exp(rng.uniform(0.0, np.log(2049))))
+        if rng.random() < 0.7:
+            sf = rng.choice([1, 2, 4, 8], size=n, p=rng.dirichlet(np.ones(4)))
+        else:
+            sf = rng.integers(1, 256, size=n)
+        c = 10.0 ** rng.uniform(-3, 3, size=n)
+        if n >= 4 and rng.random() < 0.5:
+            k = int(rng.integers(1, n // 2 + 1))
+            dst, src = rng.integers(0, n, size=k), rng.integers(0, n, size=k)
+            sf[dst], c[dst] = sf[src], c[src]
+        out.append((sf.astype(np.int32), c, G))
+    return out
+
+
+def test_twin_level_matches_lp_fuzz():
+    for sf, c, G in fuzz_instances(200, seed=5, max_n=300):
+        x, t, mu = mmf_ref.twin_allocate(sf, c, G)
+        t_lp, _ = mmf_ref.lp_level(sf, c, G)
+        assert abs(t - t_lp) <= 1e-9 * max(1.0, abs(t_lp)), (len(sf), G, t, t_lp)
+        assert float(np.dot(sf, x)) <= G * (1 + 1e-12)
+        assert np.min(c * x) >= t * (1 - 1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_mmf_fuzz_bit_exact_vs_twin(gpu_solver):
+    for i, (sf, c, G) in enumerate(fuzz_instances(300)):
+        xg, tg, mug = gpu_solver.mmf_allocate(sf, c, G)
+        xt, tt, mut = mmf_ref.twin_allocate(sf, c, G)
+        assert xg.tobytes() == xt.tobytes(), (i, len(sf), G)
+        assert np.float64(tg).tobytes() == np.float64(tt).tobytes(), (i, len(sf), G)
+        assert np.float64(mug).tobytes() == np.float64(mut).tobytes(), (i, len(sf), G)
