@@ -1,11 +1,11 @@
 """Generate tests/golden/oracle_c3.json: the reference model solved by the
-oracle (oracle/milp_ref.py, HiGHS) at the headline sizes — 8 C3 instances
-(900 jobs x 30 rounds, G=256, k=1e5, lambda=5) and 8 C5-mix instances
+oracle (oracle/milp_ref.py, HiGHS) at the headline sizes — 12 C3 instances
+(900 jobs x 30 rounds, G=256, k=1e5, lambda=5) and 16 C5-mix instances
 (900 x 30, G in {32, 64, 128, 256} with the matching scale_*gpus.json k and
 lambda) — so the GPU kernel can be checked against the ORACLE at the
 configuration the bench is quoted on, not only against the bit-exact twin.
 
-    python tests/golden/make_oracle_c3.py [--procs 6]
+    python tests/golden/make_oracle_c3.py [--procs 6] [--missing]
 
 Per instance it records (all in the maximisation sense of shockwave.py:363-379):
 
@@ -47,8 +47,8 @@ for p in (os.path.join(ROOT, "shockwave-replication_amd"), os.path.join(ROOT, "o
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle_c3.json")
 
 # (name, seed, N, G, T) — C3 seeds are disjoint from the bench's (0 … 8191 per rank)
-C3_CASES = [("c3", 500_000 + i, 900, 256, 30) for i in range(8)]
-C5_CASES = [("c5", 600_000 + i, 900, (32, 64, 128, 256)[i % 4], 30) for i in range(8)]
+C3_CASES = [("c3", 500_000 + i, 900, 256, 30) for i in range(12)]
+C5_CASES = [("c5", 600_000 + i, 900, (32, 64, 128, 256)[i % 4], 30) for i in range(16)]
 
 
 def inputs_digest(a):
@@ -143,6 +143,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=6)
     ap.add_argument("--only", default="")
+    ap.add_argument("--missing", action="store_true",
+                    help="keep the records already in the file, solve only the cases it lacks")
     ap.add_argument("--p2-only", dest="p2_only", action="store_true",
                     help="keep the P1-side oracle records, redo the twin counts and P2 MILPs")
     args = ap.parse_args()
@@ -158,8 +160,13 @@ def main():
     cases = C3_CASES + C5_CASES
     if args.only:
         cases = [c for c in cases if f"{c[0]}:{c[1]}" in args.only.split(",")]
+    have = {}
+    if args.missing and os.path.exists(OUT):
+        have = {(r["name"], r["seed"]): r for r in json.load(open(OUT))["cases"]}
+    todo = [c for c in cases if (c[0], c[1]) not in have]
     with mp.get_context("spawn").Pool(args.procs) as pool:
-        recs = pool.map(solve_case, cases, chunksize=1)
+        new = dict(zip([(c[0], c[1]) for c in todo], pool.map(solve_case, todo, chunksize=1)))
+    recs = [have.get((c[0], c[1])) or new[(c[0], c[1])] for c in cases]
     with open(OUT, "w") as f:
         json.dump({"generator": "tests/golden/make_oracle_c3.py",
                    "oracle": "oracle/milp_ref.py (HiGHS restatement of shockwave.py:281-388)",

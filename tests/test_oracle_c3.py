@@ -1,8 +1,8 @@
 """Headline-size parity against the ORACLE (oracle/milp_ref.py), not the twin.
 
-tests/golden/oracle_c3.json (tests/golden/make_oracle_c3.py) holds, for 8 C3
+tests/golden/oracle_c3.json (tests/golden/make_oracle_c3.py) holds, for 12 C3
 instances (900 jobs x 30 rounds, G=256, k=1e5, lambda=5 — the bench's
-configuration) and 8 C5-mix instances (G in {32, 64, 128, 256} with the
+configuration) and 16 C5-mix instances (G in {32, 64, 128, 256} with the
 matching scale_*gpus.json k / lambda), the reference model solved by HiGHS:
 the P1 MILP objective J_ref (shockwave.py:330-382, gap 1e-4), its LP
 relaxation bound, the smallest makespan M*, the utility term's optimum U* at
@@ -21,7 +21,7 @@ Bars (one-sided, BASELINE.json north star: within 1e-3 relative):
     on the C5 mix.
 
 The CPU test runs the twin (same algorithm, bit-exact with the GPU); the GPU
-test solves all 16 instances in ONE batched launch of the HIP kernel and
+test solves all 28 instances in ONE batched launch of the HIP kernel and
 applies the same bars to the GPU's own plans and objectives.
 """
 import hashlib
@@ -89,8 +89,8 @@ def check_against_oracle(c, a, r):
 
 
 def test_fixture_present_and_complete():
-    assert len(CASES) == 16, "tests/golden/oracle_c3.json: run tests/golden/make_oracle_c3.py"
-    assert sum(c["name"] == "c3" for c in CASES) == 8
+    assert len(CASES) == 28, "tests/golden/oracle_c3.json: run tests/golden/make_oracle_c3.py"
+    assert sum(c["name"] == "c3" for c in CASES) == 12
     assert sorted({c["G"] for c in CASES if c["name"] == "c5"}) == [32, 64, 128, 256]
     for c in CASES:
         assert c["p1"]["feasible"] and c["p1"]["status"] in ("optimal", "time_limit")
@@ -106,7 +106,7 @@ def test_twin_vs_oracle_headline(i, twin):
 
 @pytest.mark.gpu
 def test_gpu_vs_oracle_headline_one_launch(gpu_solver):
-    """All 16 headline-size instances in ONE batched launch of sw_plan_kernel
+    """All 28 headline-size instances in ONE batched launch of sw_plan_kernel
     (C3 and the C5 G-mix), each held to the oracle bars above."""
     probs = [problem(c) for c in CASES]
     rs = gpu_solver.solve_batch(probs)
@@ -118,7 +118,7 @@ def test_gpu_vs_oracle_headline_one_launch(gpu_solver):
 def test_gpu_c5_sweep_512_one_launch(gpu_solver, twin):
     """BASELINE config 5 at full size: 512 independent 900 x 30 instances
     (seeds x cluster sizes G in {32, 64, 128, 256}, k / lambda from the
-    matching scale_*gpus.json) in ONE launch of sw_plan_kernel.  The 16
+    matching scale_*gpus.json) in ONE launch of sw_plan_kernel.  The 28
     oracle-fixture instances ride in the same batch and are held to the oracle
     bars; all 512 must equal the CPU twin bit for bit and be valid plans."""
     import sw_synth as ss2
