@@ -52,7 +52,9 @@ extern "C" {
 #define SW_ERR_NOT_BUILT (-5)  /* feature not compiled into this library        */
 
 /* Result status bits (sw_result.status). */
-#define SW_STATUS_P1_REPACKED 0x1 /* aggregate P1 counts needed repair to pack */
+#define SW_STATUS_P1_REPACKED 0x1 /* aggregate P1 counts needed repair to pack
+                                     (re-solved on a smaller budget, then single
+                                     rounds added into stranded capacity) */
 #define SW_STATUS_P2_FALLBACK 0x2 /* P2 placement fell back to the P1 plan    */
 #define SW_STATUS_NO_PLANNED 0x4  /* no job has planned rounds (shockwave.py:319-320) */
 /* Which P2 placement was kept: none of these bits = the
