@@ -93,6 +93,8 @@ def main():
                 bad += 1
                 print(f"seed {c0 + i} N={a.N} G={a.G} T={a.T} k={a.k:g} nb={len(a.bases)} "
                       f"wmax={a.w.max()}: " + "; ".join(d), flush=True)
+        if (c0 + 512) % 4096 == 0:
+            print(f"... {c0 + 512} solved, {bad} differ", flush=True)
     print(f"{bad} of {n} differ ({'single' if single else 'batched'})", flush=True)
     s.close()
 
