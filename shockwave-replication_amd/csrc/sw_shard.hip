@@ -975,13 +975,13 @@ struct sw_shard_state {
     /* device */
     DevBuf<int32_t> w, F, E, l, taken, tie, arr[SW_A_COUNT], planned, porder;
     DevBuf<double> xa;
-    DevBuf<double> d, R, p, xsend, xrecv;
+    DevBuf<double> d, R, p, xrecv; /* gathers run in place: rank r's block is its send buffer */
     DevBuf<sw_jobc> jc;
     DevBuf<float> keys;
     DevBuf<uint64_t> y[SW_Y_COUNT];
     DevBuf<uint8_t> plan;
     DevBuf<long long> red, tieblk;
-    DevBuf<sw_pack_ent> psend, pall;
+    DevBuf<sw_pack_ent> pall;
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
@@ -1226,8 +1226,10 @@ int op_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
     *lb = sw_from_bits(mx[1]);
     *top = sw_from_bits(mx[3]);
     /* every job's width, gathered once (the width tail needs w of the winner) */
-    int32_t* wsend = (int32_t*)S->xsend.p;
+    /* in place: this rank's block of the receive buffer is the send buffer
+     * (no self-copy in the all-gather, none at all at world 1) */
     int32_t* wrecv = (int32_t*)S->xrecv.p;
+    int32_t* wsend = wrecv + (size_t)S->rank * S->P;
     SH_HIP(S, hipMemsetAsync(wsend, 0, (size_t)S->P * 4, st));
     if (S->NL) SH_HIP(S, hipMemcpyAsync(wsend, S->in_w, (size_t)S->NL * 4, hipMemcpyDeviceToDevice, st));
     S->w_all.resize((size_t)S->P * S->world);
@@ -1400,11 +1402,12 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     const uint64_t* ys = sel == SW_EV_FINAL ? S->y[arg].p : nullptr;
     /* lanes per block: a block's jobs (lpb lanes × q) fit its kTB threads */
     const int lpb = (int)std::max<int64_t>(1, kTB / S->q);
+    double* xs = S->xrecv.p + (size_t)S->rank * blk; /* in-place all-gather */
     if (S->q > kTB) return S->h->err = "eval: more than 256 jobs per lane", SW_ERR_CAPACITY;
     LAUNCH(S, k_eval, dim3((unsigned)((LW + lpb - 1) / lpb)), dim3(kTB), 0, S->h->stream, S->dv,
-           (int)sel, arr, ys, (int)(arg & 0xFF), (int)(arg >> 8), lpb, S->xsend.p);
+           (int)sel, arr, ys, (int)(arg & 0xFF), (int)(arg >> 8), lpb, xs);
     std::vector<double> all((size_t)blk * S->world);
-    SH_TRY(coll_gather(S, S->xsend.p, S->xrecv.p, (size_t)blk * 8, all.data()));
+    SH_TRY(coll_gather(S, xs, S->xrecv.p, (size_t)blk * 8, all.data()));
     double g = 0.0;
     int64_t s = 0;
     for (int r = 0; r < S->world; ++r) {
@@ -1448,9 +1451,10 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
         capsd = S->caps.p;
     }
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
-           (int)wc, S->psend.p);
-    const void* gv = nullptr;
-    SH_TRY(coll_gather(S, S->psend.p, S->pall.p, (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
+           (int)wc, S->pall.p + (size_t)S->rank * S->P);
+    const void* gv = nullptr; /* in-place all-gather: the keys go straight to this rank's block */
+    SH_TRY(coll_gather(S, S->pall.p + (size_t)S->rank * S->P, S->pall.p,
+                       (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
     const sw_pack_ent* all = (const sw_pack_ent*)gv;
     const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
     LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, all, M, S->skeys.p,
@@ -1534,8 +1538,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->tieblk.reserve(nblk((int64_t)NL)) ||
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
-               S->xsend.reserve(xbytes / 8 + 1) || S->xrecv.reserve((xbytes / 8 + 1) * S->world) ||
-               S->psend.reserve((size_t)S->P) || S->pall.reserve(M) ||
+               S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
                S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64) ||
                S->srch.reserve(8) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
@@ -1614,8 +1617,8 @@ void sw_shard_release(sw_handle* h) {
     S->w.release(); S->F.release(); S->E.release(); S->l.release(); S->taken.release();
     S->tie.release(); S->tieblk.release(); S->xa.release();
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
-    S->p.release(); S->xsend.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
-    S->plan.release(); S->red.release(); S->psend.release(); S->pall.release(); S->hx.release();
+    S->p.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
+    S->plan.release(); S->red.release(); S->pall.release(); S->hx.release();
     if (S->pub) (void)hipHostFree(S->pub);
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
