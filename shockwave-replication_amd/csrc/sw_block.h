@@ -367,6 +367,46 @@ struct sw_blk_t {
         M = mm;
     }
 
+    /* sw_detsum of a and of b, the max of m ≥ 0 and the sum of the small
+     * counts c, one barrier (the emit's four results) */
+    __device__ __forceinline__ void detsum2_max_cnt(double a, double b, double m, int32_t c,
+                                                    double& SA, double& SB, double& M, int64_t& C) {
+        a = wave_dettree(a);
+        b = wave_dettree(b);
+        m = wave_max_f64(m);
+        c = wave_sum_i32(c);
+        if (lane_id() == 0) {
+            X->d[par][wave_id()][0] = a;
+            X->d[par][wave_id()][1] = b;
+            X->i[par][wave_id()][0] = c;
+            X->u[par][wave_id()] = (uint64_t)__double_as_longlong(m);
+        }
+        __syncthreads();
+        double sa[NW], sb[NW];
+        double mm = __longlong_as_double((long long)X->u[par][0]);
+        int64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            sa[w] = X->d[par][w][0];
+            sb[w] = X->d[par][w][1];
+            const double mw = __longlong_as_double((long long)X->u[par][w]);
+            mm = mw > mm ? mw : mm;
+            t += X->i[par][w][0];
+        }
+#pragma unroll
+        for (int h = NW / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int i = 0; i < h; ++i) {
+                sa[i] = sa[i] + sa[i + h];
+                sb[i] = sb[i] + sb[i + h];
+            }
+        flip();
+        SA = sa[0];
+        SB = sb[0];
+        M = mm;
+        C = t;
+    }
+
     __device__ __forceinline__ double detsum(double v) {
         double S, M;
         detsum_max(v, 0.0, S, M);

@@ -1733,7 +1733,12 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         p2 = p2 + term;
         B.planned[jo + j] = cnt;
     });
-    const bool any = c.blk.sum(any_l) > 0; /* its barrier: every mask row is final */
+    /* the four emit results in one reduction; its barrier: every mask row
+     * is final */
+    double U, Mact, P2;
+    int64_t any_n;
+    c.blk.detsum2_max_cnt(fs, p2, gm, (int32_t)any_l, U, P2, Mact, any_n);
+    const bool any = any_n > 0;
     if (!any) status |= SW_STATUS_NO_PLANNED;
     /* The plan bytes (shockwave.py:390-398 reads x[j][t]): the instance's
      * N·T-byte range written with aligned 16-byte stores, each thread
@@ -1771,9 +1776,6 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             dst[ci] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
     }
-    double U, Mact;
-    c.blk.detsum_max(fs, gm, U, Mact);
-    const double P2 = c.blk.detsum(p2);
     SW_STAMP(5);
     if (threadIdx.x == 0) {
         sw_out_dev o;
