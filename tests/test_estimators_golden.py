@@ -19,7 +19,7 @@ def _cases():
         return json.load(f)["cases"]
 
 
-@pytest.mark.parametrize("ci", range(40))
+@pytest.mark.parametrize("ci", range(120))
 def test_estimator_sequence_bit_exact(ci):
     case = _cases()[ci]
     prof = case["profile"]

@@ -66,7 +66,19 @@ def _cpu_model():
     return None
 
 
+def one(mode, seed):
+    """Worker mode for bench.py's cpu_baseline leg: one timed solve (or LP
+    relaxation) of one seed, printed as one JSON line."""
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ.setdefault(k, "1")
+    dt, st, extra = (_solve if mode == "solve" else _relax)(seed)
+    print(json.dumps({"mode": mode, "seed": seed, "seconds": dt, "status": st,
+                      "p2_status" if mode == "solve" else "objective": extra}))
+
+
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] in ("--one", "--relax"):
+        return one("solve" if sys.argv[1] == "--one" else "relax", int(sys.argv[2]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=16)
     ap.add_argument("--instances", type=int, default=16)
