@@ -1,21 +1,24 @@
 #!/bin/bash
-# Round-2 evidence on the final build, one call: GPU parity suite, smoke, the
+# Evidence set for one build, one call: GPU parity suite, smoke, the
 # default bench line, rocprofv3 kernel stats of the C3 bench (no legs) and of
-# the C4 line, PMC passes at the default batch, phase stamps.
-#   gpurun --timeout 1200 -- bash tools/gpu_final_r2.sh <tag>
+# the C4 line, PMC passes at the default batch, phase stamps, the peer-transport
+# C4 timing at W = 2 / 4 as processes on one GPU.
+#   gpurun --timeout 1200 -- bash tools/gpu_evidence.sh <tag>
 set -o pipefail
-TAG=${1:-final_r2}
+TAG=${1:-evidence}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B=16384
+B=32768
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3 -o run -- python3 bench.py --no-cpu-baseline --no-legs --steps 5 --warmup 1 > $OUT/prof_c3.json 2> $OUT/prof_c3.err &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- python3 bench.py --workload c4 --steps 20 --warmup 2 > $OUT/prof_c4.json 2> $OUT/prof_c4.err &&
-bash tools/gpu_pmc_c3.sh $TAG/pmc $B &&
-timeout -k 10 200 python -u tools/stamps.py 256 > $OUT/stamps.log 2>&1
+bash tools/pmc_c3.sh $TAG/pmc $B &&
+timeout -k 10 200 python -u tools/stamps.py 256 > $OUT/stamps.log 2>&1 &&
+timeout -k 10 200 python -u tools/peer_timing.py 2 100 > $OUT/peer_w2.json 2> $OUT/peer_w2.err &&
+timeout -k 10 200 python -u tools/peer_timing.py 4 100 > $OUT/peer_w4.json 2> $OUT/peer_w4.err
 rc=$?
 echo "exit $rc"; tail -2 $OUT/pytest_gpu.log; tail -1 $OUT/smoke.log; cat $OUT/bench.json; head -14 $OUT/stamps.log
 exit $rc

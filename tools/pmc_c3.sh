@@ -2,7 +2,7 @@
 # rocprofv3 passes over the C3 bench (each its own run, kernel-trace only):
 # kernel stats, FETCH_SIZE, WRITE_SIZE, SQ counters; then, in the build container:
 #   python tools/pmc_summary.py <tag> gpurun_out/<tag>/{stats/run_kernel_stats,fetch/run_counter_collection,write/run_counter_collection,sq/run_counter_collection}.csv <batch>
-#   gpurun --timeout 600 -- bash tools/gpu_pmc_c3.sh <tag> [batch]
+#   gpurun --timeout 600 -- bash tools/pmc_c3.sh <tag> [batch]
 set -o pipefail
 TAG=${1:-pmc_c3}
 B=${2:-2048}
