@@ -241,14 +241,17 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
  * the same process), and from then on each step's all-reduce / all-gather is
  * one kernel on the handle's stream that stores this rank's partial into
  * every peer's region over xGMI and releases a sequence flag there, waits
- * (bounded: SW_ERR_RCCL after ~2 s) for every peer's flag in its own region,
- * and combines in rank order — instead of an RCCL call per step.  The
+ * (bounded: 10 s, or SW_PEER_TIMEOUT_MS from the environment at this call)
+ * for every peer's flag in its own region, and combines in rank order —
+ * instead of an RCCL call per step.  A timed-out wait returns SW_ERR_RCCL
+ * and leaves the handle unusable (the ranks stopped at different exchanges):
+ * every later solve on it returns SW_ERR_RCCL, rebuild the handle.  The
  * communicator set up by the init call is used once, to exchange the region
  * handles.  max_total_jobs bounds the instances (total_jobs) later solves
  * may pass (the regions are sized from it; larger ones return
  * SW_ERR_CAPACITY).  World 1 keeps the init call's transport.  If any rank
- * cannot allocate or map its side, every rank returns an error and keeps
- * the init call's transport.  Results are the same bits as with RCCL or host
+ * cannot allocate (fine-grained device memory is required) or map its side,
+ * every rank returns an error and keeps the init call's transport.  Results are the same bits as with RCCL or host
  * collectives.
  */
 #define SW_PEER_MAX_WORLD 64

@@ -41,7 +41,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <unistd.h>
 
@@ -850,7 +853,12 @@ __global__ __launch_bounds__(256) void k_publish(const uint32_t* src, uint32_t* 
  * it is read.  The payload is read completely before anything is combined, so
  * in-place all-reduces are safe. */
 constexpr int kXHdr = 1024;
-constexpr unsigned long long kXTimeout = 200ull * 1000 * 1000; /* wall_clock64 ticks (100 MHz): 2 s */
+/* wall_clock64 ticks (100 MHz) a rank waits for its peers' flags: 10 s by
+ * default, SW_PEER_TIMEOUT_MS overrides it (sw_dist_enable_peer).  A timeout
+ * sets the sticky error word, which makes the handle unusable: the ranks left
+ * the exchange at different sequence numbers, so every later solve on it
+ * returns SW_ERR_RCCL until the handle is rebuilt (include/shockwave_amd.h). */
+constexpr unsigned long long kXTimeoutDefault = 1000ull * 1000 * 1000;
 
 struct PeerSet {
     unsigned char* base[SW_PEER_MAX_WORLD];
@@ -864,7 +872,7 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
                                               long long half, int rank, int W, unsigned long long seq,
                                               int op, int n, unsigned char* dst, int* xerr,
                                               uint32_t* hdst, unsigned long long* hflag,
-                                              unsigned long long hseq) {
+                                              unsigned long long hseq, unsigned long long tmo) {
     const long long off = kXHdr + (long long)(seq & 1ull) * half + (long long)rank * bytes;
     if ((bytes & 15) == 0 && ((uintptr_t)src & 15) == 0) {
         const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -881,9 +889,11 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
             for (int p = 0; p < W; ++p) reinterpret_cast<unsigned long long*>(ps.base[p] + off)[i] = v;
         }
     }
-    /* the workgroup barrier orders every thread's payload stores before the
-     * flag writers' system-scope releases (release cumulativity), so one
-     * release per flag publishes the whole payload */
+    /* every thread makes its own payload stores visible at system scope
+     * before the barrier: a system-scope release orders only the issuing
+     * wave's outstanding stores, so the flag writers' releases below cannot
+     * publish the other waves' payload on their own */
+    __threadfence_system();
     __syncthreads();
     if ((int)threadIdx.x < W)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(ps.base[threadIdx.x]) + rank, seq,
@@ -895,7 +905,7 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
         const uint64_t t0 = wall_clock64();
         for (int sr = 0; sr < W && !b; ++sr)
             while (__hip_atomic_load(fl + sr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-                if (wall_clock64() - t0 > kXTimeout) { b = 1; break; }
+                if (wall_clock64() - t0 > tmo) { b = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
         if (b) atomicExch(xerr, 1);
@@ -936,6 +946,28 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
     }
 }
 
+/* A per-process identity: 128 random bits drawn once per process, and the
+ * kernel boot id (so equal nonces on two hosts cannot collide either). */
+void process_identity(unsigned long long nonce[2], char* boot, size_t boot_len) {
+    static unsigned long long n0 = 0, n1 = 0;
+    if (n0 == 0 && n1 == 0) {
+        FILE* f = fopen("/dev/urandom", "rb");
+        if (!f || fread(&n0, sizeof(n0), 1, f) != 1 || fread(&n1, sizeof(n1), 1, f) != 1) {
+            n0 = (unsigned long long)getpid() * 0x9E3779B97F4A7C15ull ^ (unsigned long long)time(nullptr);
+            n1 = (unsigned long long)(uintptr_t)&n0;
+        }
+        if (f) fclose(f);
+        if (n0 == 0 && n1 == 0) n0 = 1;
+    }
+    nonce[0] = n0;
+    nonce[1] = n1;
+    memset(boot, 0, boot_len);
+    if (FILE* b = fopen("/proc/sys/kernel/random/boot_id", "r")) {
+        if (!fgets(boot, (int)boot_len, b)) boot[0] = 0;
+        fclose(b);
+    }
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kTB - 1) / kTB > 0 ? (n + kTB - 1) / kTB : 1); }
 
 }  // namespace
@@ -967,6 +999,8 @@ struct sw_shard_state {
     unsigned long long xseq = 0;
     int* xerr = nullptr;
     int64_t xmax_jobs = 0;
+    unsigned long long xtimeout = kXTimeoutDefault;
+    bool xfailed = false;
     /* current solve */
     int32_t NL = 0, T = 0;
     int64_t N = 0, off = 0, q = 1, P = 0, LW = 0;
@@ -1072,8 +1106,10 @@ int publish_wait(sw_shard_state* S, unsigned long long seq, size_t words, size_t
             break;
         }
     }
-    if (S->pub[words] != 0u)
+    if (S->pub[words] != 0u) {
+        S->xfailed = true; /* sticky: the ranks stopped at different exchanges */
         return S->h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+    }
     memcpy(hout, S->pub, bytes);
     return SW_OK;
 }
@@ -1105,7 +1141,7 @@ int peer_xchg(sw_shard_state* S, const void* src, size_t bytes, int op, int n, v
     hipLaunchKernelGGL(k_xchg, dim3(1), dim3(256), 0, S->h->stream, S->ps, (const unsigned char*)src,
                        (long long)bytes, S->xhalf, (int)S->rank, (int)S->world, ++S->xseq, op, n,
                        (unsigned char*)dst, S->xerr, hout ? S->pub_dev : nullptr,
-                       hout ? S->pub_flag_dev : nullptr, hseq);
+                       hout ? S->pub_flag_dev : nullptr, hseq, S->xtimeout);
     SH_HIP(S, hipGetLastError());
     if (hout) return publish_wait(S, hseq, obytes / 4, obytes, hout);
     return SW_OK;
@@ -1734,25 +1770,37 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
     const long long slot = peer_slot_bytes(max_total_jobs, W);
     const long long half = slot * W;
     const size_t bytes = (size_t)kXHdr + 2 * (size_t)half;
-    /* every rank: {ok, pid, region pointer, IPC handle}.  A local failure is
-     * carried through both all-gathers instead of returning early, so that
-     * every rank reaches them and all ranks keep the init call's transport
-     * together when any rank could not set up its side. */
+    /* every rank: {ok, process identity, device, region pointer, IPC handle}.
+     * A local failure is carried through both all-gathers instead of
+     * returning early, so that every rank reaches them and all ranks keep the
+     * init call's transport together when any rank could not set up its side.
+     * Process identity = a per-process random nonce (drawn once) plus the
+     * kernel's boot id: ranks in different containers can share a PID, never
+     * both of these, so the raw-pointer path is taken only inside one process. */
     struct Rec {
-        long long ok, pid;
+        long long ok, device;
+        unsigned long long nonce[2];
+        char boot[40];
         unsigned long long ptr;
         hipIpcMemHandle_t ih;
     };
     Rec mine;
     memset(&mine, 0, sizeof(mine));
-    mine.pid = (long long)getpid();
+    process_identity(mine.nonce, mine.boot, sizeof(mine.boot));
+    mine.device = h->device;
+    if (const char* e = getenv("SW_PEER_TIMEOUT_MS")) {
+        const long long ms = atoll(e);
+        if (ms > 0) S->xtimeout = (unsigned long long)ms * 100000ull;
+    }
     {
         /* fine-grained device memory: peers write it over xGMI, and this
-         * GPU's L2 must not hold stale copies of those lines */
+         * GPU's L2 must not hold stale copies of those lines.  Coarse-grained
+         * memory could serve stale lines, so without fine-grained memory the
+         * setup fails and every rank keeps the init transport. */
         void* reg = nullptr;
         if (hipExtMallocWithFlags(&reg, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
             (void)hipGetLastError();
-            if (hipMalloc(&reg, bytes) != hipSuccess) reg = nullptr;
+            reg = nullptr;
         }
         S->xreg = (unsigned char*)reg;
         bool ok = reg != nullptr && hipMemset(reg, 0, bytes) == hipSuccess &&
@@ -1773,7 +1821,18 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
     for (int32_t p = 0; p < W && ok; ++p) {
         if (p == S->rank) {
             S->ps.base[p] = S->xreg;
-        } else if (all[(size_t)p].pid == mine.pid) { /* same process: the pointer itself */
+        } else if (all[(size_t)p].nonce[0] == mine.nonce[0] && all[(size_t)p].nonce[1] == mine.nonce[1] &&
+                   memcmp(all[(size_t)p].boot, mine.boot, sizeof(mine.boot)) == 0) {
+            /* same process: the pointer itself; another device needs peer access */
+            if (all[(size_t)p].device != mine.device) {
+                const hipError_t pe = hipDeviceEnablePeerAccess((int)all[(size_t)p].device, 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                    (void)hipGetLastError();
+                    ok = 0;
+                    break;
+                }
+                (void)hipGetLastError();
+            }
             S->ps.base[p] = (unsigned char*)(uintptr_t)all[(size_t)p].ptr;
         } else {
             void* q = nullptr;
@@ -1829,6 +1888,9 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     if (hipSetDevice(h->device) != hipSuccess) return h->err = "hipSetDevice", SW_ERR_HIP;
     if (S->peer && total_jobs > S->xmax_jobs)
         return h->err = "total_jobs exceeds sw_dist_enable_peer's max_total_jobs", SW_ERR_CAPACITY;
+    if (S->peer && S->xfailed)
+        return h->err = "peer exchange timed out earlier: the ranks' sequence numbers diverged, "
+                        "rebuild the handle", SW_ERR_RCCL;
     SH_TRY(prepare(S, local, job_offset, total_jobs, dev, res));
     sw_shard_ops ops;
     ops.ctx = S;
@@ -1867,7 +1929,10 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     if (S->peer) { /* a timed-out exchange after the last publish */
         int e = 0;
         SH_HIP(S, hipMemcpy(&e, S->xerr, sizeof(int), hipMemcpyDeviceToHost));
-        if (e) return h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+        if (e) {
+            S->xfailed = true; /* sticky: the handle is unusable from here on */
+            return h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+        }
     }
     return rc;
 }

@@ -4,7 +4,11 @@ sw_dist_enable_peer so that every step's collective goes through the other
 process's IPC-mapped exchange region.  Writes this rank's rows and the global
 scalars of each case to <outdir>/c<case>_r<rank>.npz.
 
-    python tests/peer_worker.py <rank> <world> <port> <outdir> <cases.json>
+    python tests/peer_worker.py <rank> <world> <port> <outdir> <cases.json> [late]
+
+"late": rank 1 enters the first solve 1.5 s after rank 0, with a 300 ms peer
+timeout (SW_PEER_TIMEOUT_MS); each rank records the outcome of that solve and
+of one more solve on the same handle to <outdir>/late_r<rank>.json.
 """
 import json
 import os
@@ -28,10 +32,34 @@ def main():
     import sw_native as sn
     import sw_synth as ss
 
+    late = len(sys.argv) > 6 and sys.argv[6] == "late"
+    if late:
+        os.environ["SW_PEER_TIMEOUT_MS"] = "300"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     s = sn.Solver(device=0)
     s.dist_init_host(sn.HostComm(sn.TorchGroupComm()), rank, world)
     s.dist_enable_peer(max(c[1] for c in cases))
+    if late:
+        import time
+
+        seed, N, G, T, k, lam = cases[0]
+        a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+        lo, hi = sn.shard_range(a.N, world, rank)
+        out = []
+        dist.barrier()
+        if rank == 1:
+            time.sleep(1.5)
+        for _ in range(2):
+            try:
+                r = s.dist_solve(a.slice(lo, hi), lo, a.N)
+                out.append(["ok", int(r["rc"])])
+            except sn.NativeError as e:
+                out.append(["error", str(e)])
+        json.dump(out, open(os.path.join(outdir, f"late_r{rank}.json"), "w"))
+        s.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     for ci, (seed, N, G, T, k, lam) in enumerate(cases):
         a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
         lo, hi = sn.shard_range(a.N, world, rank)

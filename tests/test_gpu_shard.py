@@ -172,6 +172,39 @@ def test_gpu_shard_peer_transport_two_processes(tmp_path, twin):
         assert_same_as_single(rs, twin.solve(a), f"peer W=2 {case}")
 
 
+def test_gpu_shard_peer_late_rank_fails_cleanly(tmp_path):
+    """A rank that enters a solve after its peers' exchange timeout: both
+    ranks get SW_ERR_RCCL (no hang), and the handle then stays unusable —
+    the next solve on it fails at once instead of exchanging with sequence
+    numbers that no longer agree (include/shockwave_amd.h, sw_dist_enable_peer)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cj = tmp_path / "cases.json"
+    cj.write_text(json.dumps([list(CASES[1])]))
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "peer_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", str(port), str(tmp_path), str(cj),
+                               "late"]) for r in range(2)]
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=120))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(None)
+    assert rcs == [0, 0], rcs
+    for r in range(2):
+        out = json.load(open(tmp_path / f"late_r{r}.json"))
+        assert out[0][0] == "error" and "timed out" in out[0][1], (r, out)
+        assert out[1][0] == "error" and "rebuild the handle" in out[1][1], (r, out)
+
+
 def test_gpu_shard_fuzz_rccl_world1(rccl_solver, twin):
     """The sharded engine over 256 fuzz instances (tests/fuzzcases.py)."""
     from fuzzcases import fuzz_problem
