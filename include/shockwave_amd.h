@@ -62,6 +62,9 @@ extern "C" {
 #define SW_STATUS_P2_WEIGHT_ORDER 0x8 /* the weight order p_j/n_j placed every round   */
 #define SW_STATUS_P2_CLASSWISE 0x10   /* width classes repacked inside the P1 profile  */
 #define SW_STATUS_P2_REPAIRED 0x20    /* density order with its width profile repaired */
+/* The exchange step (negative-cycle cancelling over round moves, DESIGN.md
+ * §3.6) improved the kept P2 placement. */
+#define SW_STATUS_P2_EXCHANGED 0x40
 
 /*
  * One plan solve.  Field ↔ reference:

@@ -1,0 +1,282 @@
+/*
+ * oracle/p2x_twin.c — TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+ *
+ * Sequential specification of the P2 exchange step (negative-cycle
+ * cancelling over round moves, csrc/sw_p2x.h) that the GPU
+ * kernel (csrc/sw_p2x_kernel.hip) and the sharded engine run in parallel.
+ * The plan twin (plan_twin.c) calls it on its final P2 placement and the CPU
+ * shard engine (shard_twin.c) on the gathered placement; the GPU must return
+ * the same masks bit for bit.  Reference: the P2 MILP, shockwave.py:281-328.
+ *
+ * Layout.  Active jobs (n_j > 0) are grouped by width class (classes in
+ * ascending width), and inside a class ranked by (c desc, job asc) with
+ * c = p/n.  Position p = off[k] + rank.  Class k's membership of round t is
+ * a bitset over its ranks, nw[k] words at B + boff[k] + t·nw[k].
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/shockwave_amd.h"
+#include "../shockwave-replication_amd/csrc/sw_p2x.h"
+
+double twin_detsum(const double* v, int32_t N); /* plan_twin.c */
+
+typedef struct {
+    int32_t job;
+    double c;
+} p2x_ent;
+
+static int ent_cmp(const void* a, const void* b) {
+    const p2x_ent* x = (const p2x_ent*)a;
+    const p2x_ent* y = (const p2x_ent*)b;
+    if (x->c != y->c) return x->c > y->c ? -1 : 1;
+    return x->job < y->job ? -1 : (x->job > y->job);
+}
+
+typedef struct {
+    int32_t T, G, K, A;
+    int32_t wc[SW_P2X_KMAX], M[SW_P2X_KMAX], off[SW_P2X_KMAX], nw[SW_P2X_KMAX], boff[SW_P2X_KMAX];
+    int32_t* pjob;  /* [A] job of position p          */
+    double* pc;     /* [A] c of position p            */
+    uint64_t* pm;   /* [A] round mask of position p   */
+    uint64_t* B;    /* class × round rank bitsets     */
+    int32_t room[SW_TMAX];
+    double W[SW_TMAX * SW_TMAX]; /* W[t·T + u], δ included; SW_P2X_NONE = no edge */
+    int8_t Wk[SW_TMAX * SW_TMAX]; /* class of the edge                         */
+} p2x_t;
+
+static uint64_t* bits(p2x_t* X, int32_t k, int32_t t) { return X->B + X->boff[k] + (size_t)t * X->nw[k]; }
+
+/* W for load size F: per edge the cheapest class (ascending class on ties). */
+static void build_w(p2x_t* X, int32_t F, double delta) {
+    const int32_t T = X->T;
+    for (int32_t t = 0; t < T; ++t) {
+        for (int32_t u = 0; u < T; ++u) {
+            double best = SW_P2X_NONE;
+            int32_t bk = -1;
+            if (u != t) {
+                for (int32_t k = 0; k < X->K; ++k) {
+                    if (X->wc[k] > F || F % X->wc[k] != 0) continue;
+                    const double cost = sw_p2x_cost(bits(X, k, t), bits(X, k, u), X->nw[k], F / X->wc[k],
+                                                    t, u, X->pc + X->off[k]);
+                    if (cost < best) { best = cost; bk = k; }
+                }
+            }
+            X->W[t * T + u] = bk >= 0 ? best + delta : SW_P2X_NONE;
+            X->Wk[t * T + u] = (int8_t)bk;
+        }
+    }
+}
+
+/* Bellman–Ford (Jacobi) over rounds 0..T−1 and V = T; *len nodes of a
+ * negative cycle into cyc (in predecessor order: cyc[i+1] = pred(cyc[i])),
+ * 0 when there is none. */
+static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
+    const int32_t T = X->T;
+    double d[SW_TMAX + 1], nd[SW_TMAX + 1];
+    int32_t pr[SW_TMAX + 1], np[SW_TMAX + 1];
+    for (int32_t x = 0; x <= T; ++x) { d[x] = 0.0; pr[x] = -1; }
+    for (int32_t it = 0; it <= T; ++it) {
+        int changed = 0;
+        for (int32_t u = 0; u < T; ++u) {
+            double best = d[u];
+            int32_t bp = pr[u];
+            for (int32_t t = 0; t < T; ++t) {
+                const double w = X->W[t * T + u];
+                if (t == u || !(w < SW_P2X_NONE)) continue;
+                const double v = d[t] + w;
+                if (v < best) { best = v; bp = t; }
+            }
+            if (d[T] < best) { best = d[T]; bp = T; } /* V → u, cost 0 */
+            nd[u] = best;
+            np[u] = bp;
+            changed |= best < d[u];
+        }
+        {
+            double best = d[T];
+            int32_t bp = pr[T];
+            for (int32_t t = 0; t < T; ++t)
+                if (X->room[t] >= F && d[t] < best) { best = d[t]; bp = t; } /* t → V, cost 0 */
+            nd[T] = best;
+            np[T] = bp;
+            changed |= best < d[T];
+        }
+        if (!changed) return 0;
+        for (int32_t x = 0; x <= T; ++x) { d[x] = nd[x]; pr[x] = np[x]; }
+        /* a cycle of the predecessor graph: T + 1 steps from x still defined */
+        for (int32_t x = 0; x <= T; ++x) {
+            int32_t y = x;
+            for (int32_t s = 0; s <= T && y >= 0; ++s) y = pr[y];
+            if (y < 0) continue;
+            int32_t len = 0, v = y;
+            do { cyc[len++] = v; v = pr[v]; } while (v != y);
+            /* its exact cost, in this order (edges pred(v) → v) */
+            double cost = 0.0;
+            for (int32_t i = 0; i < len; ++i) {
+                const int32_t u = cyc[i], t = pr[u];
+                if (u < T && t < T) cost = cost + X->W[t * T + u];
+            }
+            return cost < 0.0 ? len : 0;
+        }
+    }
+    return 0;
+}
+
+/* Moves the selections of every edge of the cycle (all selected first, from
+ * the state before the cycle, then applied). */
+static void cancel(p2x_t* X, int32_t F, const int32_t* cyc, int32_t len, int32_t* tmp) {
+    const int32_t T = X->T;
+    int32_t nsel = 0;
+    for (int32_t i = 0; i < len; ++i) {
+        const int32_t u = cyc[i], t = cyc[(i + 1) % len]; /* pred(u) = t */
+        if (u == T || t == T) continue;
+        const int32_t k = X->Wk[t * T + u];
+        const int32_t q = F / X->wc[k];
+        int32_t r = sw_p2x_start(bits(X, k, t), bits(X, k, u), X->nw[k], q, u < t);
+        for (int32_t g = 0; g < q; ++g) {
+            tmp[nsel++] = (k << 24) | (t << 16) | (u << 8);
+            tmp[nsel++] = r;
+            if (g + 1 < q) r = sw_p2x_next(bits(X, k, t), bits(X, k, u), X->nw[k], r + 1);
+        }
+    }
+    for (int32_t i = 0; i < nsel; i += 2) {
+        const int32_t k = tmp[i] >> 24, t = (tmp[i] >> 16) & 0xFF, u = (tmp[i] >> 8) & 0xFF;
+        const int32_t r = tmp[i + 1];
+        bits(X, k, t)[r >> 6] &= ~(1ull << (r & 63));
+        bits(X, k, u)[r >> 6] |= 1ull << (r & 63);
+        X->pm[X->off[k] + r] ^= (1ull << t) | (1ull << u);
+        X->room[t] += X->wc[k];
+        X->room[u] -= X->wc[k];
+    }
+}
+
+/*
+ * The exchange step on the active jobs (ascending job order): job[i], w[i],
+ * c[i] = p/n, m[i] (round mask, improved in place).  Returns the number of
+ * cycles cancelled; 0 (no change) when there are more than SW_P2X_KMAX
+ * width classes.
+ */
+int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const int32_t* w,
+                     const double* c, uint64_t* m) {
+    if (A <= 0 || T < 2) return 0;
+    p2x_t* X = (p2x_t*)calloc(1, sizeof(p2x_t));
+    X->T = T;
+    X->G = G;
+    for (int32_t i = 0; i < A; ++i) {
+        int32_t k = 0;
+        while (k < X->K && X->wc[k] != w[i]) ++k;
+        if (k == X->K) {
+            if (X->K == SW_P2X_KMAX) { free(X); return 0; }
+            X->wc[X->K++] = w[i];
+        }
+    }
+    /* classes ascending */
+    for (int32_t a = 1; a < X->K; ++a)
+        for (int32_t b = a; b > 0 && X->wc[b - 1] > X->wc[b]; --b) {
+            const int32_t s = X->wc[b]; X->wc[b] = X->wc[b - 1]; X->wc[b - 1] = s;
+        }
+    X->A = A;
+    X->pjob = (int32_t*)malloc(sizeof(int32_t) * A);
+    X->pc = (double*)malloc(sizeof(double) * A);
+    X->pm = (uint64_t*)malloc(sizeof(uint64_t) * A);
+    p2x_ent* e = (p2x_ent*)malloc(sizeof(p2x_ent) * A);
+    int32_t p = 0, nb = 0;
+    for (int32_t k = 0; k < X->K; ++k) {
+        int32_t M = 0;
+        for (int32_t i = 0; i < A; ++i)
+            if (w[i] == X->wc[k]) { e[M].job = job[i]; e[M].c = c[i]; ++M; }
+        qsort(e, (size_t)M, sizeof(p2x_ent), ent_cmp);
+        X->M[k] = M;
+        X->off[k] = p;
+        X->nw[k] = (M + 63) / 64;
+        X->boff[k] = nb;
+        nb += X->nw[k] * T;
+        for (int32_t r = 0; r < M; ++r) {
+            X->pjob[p + r] = e[r].job;
+            X->pc[p + r] = e[r].c;
+        }
+        p += M;
+    }
+    /* masks by position (the job ids are unique) */
+    for (int32_t q = 0; q < A; ++q) {
+        int32_t lo = 0, hi = A - 1; /* job is ascending in the input */
+        const int32_t jq = X->pjob[q];
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) / 2;
+            if (job[mid] < jq) lo = mid + 1; else hi = mid;
+        }
+        X->pm[q] = m[lo];
+    }
+    X->B = (uint64_t*)calloc((size_t)(nb > 0 ? nb : 1), sizeof(uint64_t));
+    for (int32_t t = 0; t < T; ++t) X->room[t] = G;
+    double* v = (double*)malloc(sizeof(double) * A);
+    for (int32_t k = 0; k < X->K; ++k)
+        for (int32_t r = 0; r < X->M[k]; ++r) {
+            const int32_t q = X->off[k] + r;
+            int64_t S = 0;
+            for (int32_t t = 0; t < T; ++t)
+                if ((X->pm[q] >> t) & 1ull) {
+                    bits(X, k, t)[r >> 6] |= 1ull << (r & 63);
+                    X->room[t] -= X->wc[k];
+                    S += t;
+                }
+            v[q] = X->pc[q] * (double)S;
+        }
+    const double delta = SW_P2X_EPS * twin_detsum(v, A) / (double)T;
+    int32_t cyc[SW_TMAX + 1];
+    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)(SW_TMAX + 1) * SW_MAX_WIDTH);
+    int32_t ncancel = 0;
+    for (int changed = 1; changed && ncancel < SW_P2X_MAX_CANCEL;) {
+        changed = 0;
+        for (int32_t ki = 0; ki < X->K && ncancel < SW_P2X_MAX_CANCEL; ++ki) {
+            const int32_t F = X->wc[ki];
+            while (ncancel < SW_P2X_MAX_CANCEL) {
+                build_w(X, F, delta);
+                const int32_t len = find_cycle(X, F, cyc);
+                if (len == 0) break;
+                cancel(X, F, cyc, len, tmp);
+                ++ncancel;
+                changed = 1;
+            }
+        }
+    }
+    /* back to the input order */
+    for (int32_t q = 0; q < A; ++q) {
+        int32_t lo = 0, hi = A - 1;
+        const int32_t jq = X->pjob[q];
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) / 2;
+            if (job[mid] < jq) lo = mid + 1; else hi = mid;
+        }
+        m[lo] = X->pm[q];
+    }
+    free(tmp); free(v); free(e);
+    free(X->pjob); free(X->pc); free(X->pm); free(X->B); free(X);
+    return ncancel;
+}
+
+/* The step on a full plan (y: [N][T] bytes, counts n): used by the plan twin. */
+int32_t twin_p2x_plan(int32_t N, int32_t T, int32_t G, const int32_t* w, const double* prio,
+                      const int32_t* n, uint8_t* y) {
+    int32_t A = 0;
+    for (int32_t j = 0; j < N; ++j) A += n[j] > 0;
+    if (A == 0) return 0;
+    int32_t* job = (int32_t*)malloc(sizeof(int32_t) * A);
+    int32_t* wa = (int32_t*)malloc(sizeof(int32_t) * A);
+    double* c = (double*)malloc(sizeof(double) * A);
+    uint64_t* m = (uint64_t*)malloc(sizeof(uint64_t) * A);
+    int32_t i = 0;
+    for (int32_t j = 0; j < N; ++j) {
+        if (n[j] <= 0) continue;
+        uint64_t mk = 0;
+        for (int32_t t = 0; t < T; ++t) mk |= (uint64_t)(y[(size_t)j * T + t] != 0) << t;
+        job[i] = j; wa[i] = w[j]; c[i] = prio[j] / (double)n[j]; m[i] = mk;
+        ++i;
+    }
+    const int32_t nc = twin_p2x_run(A, T, G, job, wa, c, m);
+    for (i = 0; i < A; ++i)
+        for (int32_t t = 0; t < T; ++t) y[(size_t)job[i] * T + t] = (uint8_t)((m[i] >> t) & 1ull);
+    free(job); free(wa); free(c); free(m);
+    return nc;
+}

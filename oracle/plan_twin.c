@@ -71,6 +71,11 @@ static double sw_detsum(const double* v, int32_t N) {
     return wsum[0];
 }
 
+double twin_detsum(const double* v, int32_t N) { return sw_detsum(v, N); }
+
+int32_t twin_p2x_plan(int32_t N, int32_t T, int32_t G, const int32_t* w, const double* prio,
+                      const int32_t* n, uint8_t* y); /* p2x_twin.c */
+
 static double fval(const twin_t* P, int32_t j, int32_t n) {
     return sw_f(&P->jc[j], n, P->nb, P->beta, P->ell, P->slope);
 }
@@ -789,6 +794,10 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
         free(yc);
         if (ok2) status |= SW_STATUS_P2_CLASSWISE;
     }
+    /* the exchange step (sw_p2x.h) on a P2 placement that
+     * placed every round; a fallback keeps P1's x untouched (:325-326) */
+    if (ok2 && twin_p2x_plan(N, T, P.G, pr->nworkers, pr->priority, nb, y2) > 0)
+        status |= SW_STATUS_P2_EXCHANGED;
     uint8_t* yf = y2;
     if (!ok2) { yf = y1; status |= SW_STATUS_P2_FALLBACK; }
     free(k1); free(k2); free(nbest);

@@ -425,6 +425,50 @@ static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_
     return 0;
 }
 
+/* the P2 exchange step on the gathered placement (twin_p2x_run) */
+int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const int32_t* w,
+                     const double* c, uint64_t* m);
+typedef struct {
+    uint64_t m;
+    double p;
+    int32_t n, pad;
+} p2g_t;
+
+static int e_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
+    eng_t* E = (eng_t*)ctx;
+    const int64_t P = E->P > 0 ? E->P : 1, N = E->N;
+    p2g_t* mine = (p2g_t*)calloc((size_t)P, sizeof(p2g_t));
+    p2g_t* all = (p2g_t*)calloc((size_t)P * E->world, sizeof(p2g_t));
+    int32_t* job = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    int32_t* w = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    double* c = (double*)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+    uint64_t* m = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(N > 0 ? N : 1));
+    int rc = -1;
+    if (!mine || !all || !job || !w || !c || !m) goto out;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        mine[i].n = E->arr[nsrc][i];
+        mine[i].p = E->p[i];
+        mine[i].m = E->y[ysrc][i];
+    }
+    rc = E->comm->allgather(E->comm->ctx, mine, all, P * (int64_t)sizeof(p2g_t));
+    if (rc) goto out;
+    int32_t A = 0;
+    for (int64_t j = 0; j < N; ++j) { /* blocks are P long and contiguous: job j at j */
+        if (all[j].n <= 0) continue;
+        job[A] = (int32_t)j;
+        w[A] = E->w_all[j];
+        c[A] = all[j].p / (double)all[j].n;
+        m[A] = all[j].m;
+        ++A;
+    }
+    *cancels = twin_p2x_run(A, E->T, E->G, job, w, c, m);
+    for (int32_t a = 0; a < A; ++a)
+        if (job[a] >= E->off && job[a] < E->off + E->NL) E->y[ysrc][job[a] - E->off] = m[a];
+out:
+    free(mine); free(all); free(job); free(w); free(c); free(m);
+    return rc;
+}
+
 /*
  * One rank's sharded solve (same contract as sw_dist_plan_solve): `local`
  * holds this rank's jobs, [job_offset, job_offset + local->num_jobs) of
@@ -493,6 +537,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.pack_class = e_pack_class;
     ops.fill_best = e_fill_best;
     ops.fill_apply = e_fill_apply;
+    ops.p2x = e_p2x;
     ops.search = NULL; /* the controller's own K-ary loop */
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,

@@ -1,0 +1,109 @@
+/*
+ * sw_p2x.h — P2 exchange step: negative-cycle cancelling over round moves
+ * (DESIGN.md §3.6).  Plain C99 + HIP qualifiers; the constants and the
+ * per-edge selection are shared by the GPU kernel (sw_p2x_kernel.hip, one
+ * workgroup per instance), the sharded engine and the CPU twin
+ * (oracle/p2x_twin.c, the sequential specification).
+ *
+ * The reference's P2 (shockwave.py:281-328) is the MILP
+ *     min Σ_j (p_j/n_j)·Σ_t t·y_jt   s.t.  Σ_t y_jt = n_j,  Σ_j w_j·y_jt ≤ G,
+ * solved by Gurobi at MIPGap 1e-3.  The placement cascade (density order,
+ * width-profile repair, ...) lands within a few percent of its optimum; this
+ * step closes the rest.  With c_j = p_j/n_j, moving job j from round t to
+ * round u changes the objective by c_j·(u − t).  For a load size F (each
+ * class width present), the ROUND GRAPH has an edge t → u whose cost is the
+ * cheapest way to move exactly F GPUs of load from t to u with jobs of ONE
+ * class k (w_k | F): the q = F/w_k class-k jobs in t but not in u with the
+ * largest c (u < t: they gain) or the smallest c (u > t: they lose).  A
+ * virtual node V stands for free capacity: t → V is allowed when round t has
+ * F free GPUs (t absorbs the load), V → u always (u's load leaves).  Every
+ * cycle of this graph keeps every round's load and every job's count, so a
+ * negative cycle is an improving move of several jobs at once (one wide job
+ * against several narrow ones, chains of shifted rounds, ...).  A job can be
+ * picked on two edges of one simple cycle only as a net move between two
+ * other rounds, so cycles never conflict.  Inside one width class with no
+ * free capacity this is exact: the class's placement is a transportation
+ * problem, optimal iff its residual graph has no negative cycle.
+ *
+ * Cycles are found by Bellman–Ford (Jacobi sweeps, a cycle check of the
+ * predecessor graph after each sweep) on edge costs shifted by δ = ε·P2₀/T
+ * (P2₀ the objective before the step): a cycle is cancelled only if it
+ * gains more than δ per edge, which bounds the number of cancels; at most
+ * SW_P2X_MAX_CANCEL are applied.  Measured against the HiGHS optimum of the
+ * reference P2 on the simulator-captured and headline fixtures: ≤ 1.0014×
+ * (tests/test_p2.py, tests/test_oracle_c3.py).
+ */
+#ifndef SW_P2X_H
+#define SW_P2X_H
+
+#include <stdint.h>
+
+#include "sw_arith.h"
+
+#define SW_P2X_EPS 1e-4        /* δ = ε·P2₀/T per edge                          */
+#define SW_P2X_MAX_CANCEL 256  /* cancels per solve                              */
+#define SW_P2X_KMAX 8          /* width classes handled (more: the step is skipped) */
+#define SW_P2X_NONE 1.0e300    /* "no edge" cost                                 */
+
+/* The ranks the edge t → u moves in one class: X = Bt & ~Bu over the class's
+ * rank bitset (nw words; rank r = bit r % 64 of word r / 64, ranks in
+ * (c desc, job asc) order) — the q lowest ranks of X when lo (u < t: the
+ * largest c), else its q highest.  sw_p2x_start returns the lowest selected
+ * rank (-1 when X has fewer than q ranks: no edge for this class);
+ * sw_p2x_next(r) the smallest rank ≥ r of X, so the selection is start,
+ * next(start + 1), ... (q ranks, ascending). */
+SW_HD int32_t sw_p2x_start(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t q,
+                           int32_t lo) {
+    int32_t acc = 0;
+    if (lo) {
+        for (int32_t i = 0; i < nw; ++i) {
+            const uint64_t x = Bt[i] & ~Bu[i];
+            if (x) {
+                int32_t tot = acc;
+                for (int32_t k = i; k < nw && tot < q; ++k)
+                    tot += __builtin_popcountll(Bt[k] & ~Bu[k]);
+                return tot >= q ? 64 * i + __builtin_ctzll(x) : -1;
+            }
+        }
+        return -1;
+    }
+    for (int32_t i = nw - 1; i >= 0; --i) {
+        uint64_t x = Bt[i] & ~Bu[i];
+        const int32_t cnt = __builtin_popcountll(x);
+        if (acc + cnt >= q) {
+            /* keep the (q − acc) highest bits of x: drop its lowest ones */
+            for (int32_t d = cnt - (q - acc); d > 0; --d) x &= x - 1;
+            return 64 * i + __builtin_ctzll(x);
+        }
+        acc += cnt;
+    }
+    return -1;
+}
+
+SW_HD int32_t sw_p2x_next(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t r) {
+    int32_t i = r >> 6;
+    if (i >= nw) return -1;
+    uint64_t x = (Bt[i] & ~Bu[i]) & (~0ull << (r & 63));
+    while (!x) {
+        if (++i >= nw) return -1;
+        x = Bt[i] & ~Bu[i];
+    }
+    return 64 * i + __builtin_ctzll(x);
+}
+
+/* Cost of the class's edge: Σ c over the selected ranks (ascending) times
+ * (u − t); SW_P2X_NONE when the class has no such edge.  c is the class's
+ * c array indexed by rank. */
+SW_HD double sw_p2x_cost(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t q, int32_t t,
+                         int32_t u, const double* c) {
+    int32_t r = sw_p2x_start(Bt, Bu, nw, q, u < t);
+    if (r < 0) return SW_P2X_NONE;
+    double s = 0.0;
+    for (int32_t g = 0; g < q; ++g) {
+        s = s + c[r];
+        if (g + 1 < q) r = sw_p2x_next(Bt, Bu, nw, r + 1);
+    }
+    return s * (double)(u - t);
+}
+
+#endif /* SW_P2X_H */

@@ -124,6 +124,10 @@ typedef struct sw_shard_ops {
      * to its arr[SW_A_NFIN] on the owning rank */
     int (*fill_best)(void* ctx, const int64_t* load, uint64_t* best);
     int (*fill_apply)(void* ctx, int64_t jb, int32_t t);
+    /* the P2 exchange step (sw_p2x.h) on the placement Y[ysrc] of the counts
+     * arr[nsrc]: the active jobs' rows are gathered, the step runs on every
+     * rank alike and each rank keeps its own rows; *cancels = cycles applied */
+    int (*p2x)(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels);
     /* optional (NULL = the controller drives count_gt / feasible itself):
      * the whole K-ary search of swc_search inside the engine — kind 0 over
      * count_gt, 1 over feasible — returning its answer and the number of
@@ -577,6 +581,12 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             if (ok2) status |= SW_STATUS_P2_CLASSWISE;
         }
         if (!ok2) status |= SW_STATUS_P2_FALLBACK;
+        if (ok2) { /* the exchange step (twin: twin_p2x_plan) */
+            int32_t nc = 0;
+            SWC_RUN(o->p2x(o->ctx, SW_Y_2, SW_A_NFIN, &nc));
+            c->steps++;
+            if (nc > 0) status |= SW_STATUS_P2_EXCHANGED;
+        }
         int64_t any;
         SWC_RUN(o->eval(o->ctx, SW_EV_FINAL, ok2 ? SW_Y_2 : SW_Y_BEST, c->lanesA, c->lanesB, &gm,
                         &any));

@@ -5,7 +5,8 @@ configurations (scale_{32,64,128,256}gpus.json's k and lambda).
 History: first pinned with the plain price bisection (commit aed1d81), kept
 through the snapped searches (same results); re-pinned in
 round 2 when the P2 cascade gained the width-profile repair (sw_repair.h),
-which changes placements on purpose.  Performance-only changes must keep
+which changes placements on purpose, and in round 3 when P2 gained the
+exchange step (sw_p2x.h, negative-cycle cancelling).  Performance-only changes must keep
 these digests; tests/test_twin_plans.py checks the twin and the GPU kernel
 against them.  Regenerate only when the algorithm is meant to change:
 

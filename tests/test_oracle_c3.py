@@ -15,10 +15,11 @@ Bars (one-sided, BASELINE.json north star: within 1e-3 relative):
   * (J_lp - J) / |J| <= 1e-3: the LP relaxation bound certifies J;
   * when k >= 1 (makespan-dominated): M == M* and U >= U* - 1e-3 |U*|,
     U <= the certified dual bound of the utility problem;
-  * P2 objective <= P2_MILP * (1 + 1e-2): the reference solves P2 as a MILP
-    at gap 1e-3; the placement here is the density order with its width
-    profile repaired (sw_repair.h), measured at <= 1.0016x at C3 and <= 1.0054x
-    on the C5 mix.
+  * P2 objective <= P2_MILP * (1 + 2e-3): the reference solves P2 as a MILP
+    at gap 1e-3; the placement here is the density order (width profile
+    repaired where it strands rounds, sw_repair.h) followed by the exchange
+    step (sw_p2x.h), measured at <= 1.0002x on all 28 instances (<= 1.0054x
+    before the exchange step).
 
 The CPU test runs the twin (same algorithm, bit-exact with the GPU); the GPU
 test solves all 28 instances in ONE batched launch of the HIP kernel and
@@ -37,7 +38,7 @@ from helpers import check_plan_valid, to_oracle
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_c3.json")
 REL = 1e-3
-P2_TOL = 1e-2
+P2_TOL = 2e-3
 
 
 def _cases():
