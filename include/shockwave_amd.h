@@ -175,10 +175,11 @@ void* sw_stream(sw_handle* h);
  * Per-kernel timing with HIP events recorded on the handle's stream around
  * each launch of sw_batch_run.  enable=1 turns it on (adds two event records
  * per kernel).  sw_kernel_times() synchronises and returns accumulated ms for
- * [0] the row-build kernel and [1] the plan kernel, plus the number of runs.
+ * [0] the P2 exchange kernel (sw_p2x_kernel) and [1] the plan kernel
+ * (sw_plan_kernel), plus the number of runs.
  */
 int sw_set_timing(sw_handle* h, int32_t enable);
-int sw_kernel_times(sw_handle* h, double* ms_rows, double* ms_plan, int32_t* runs);
+int sw_kernel_times(sw_handle* h, double* ms_p2x, double* ms_plan, int32_t* runs);
 
 /*
  * Sharded single instance (jobs split across ranks, one process per GPU;

@@ -27,10 +27,12 @@ typedef struct {
     double c;
 } p2x_ent;
 
+/* (sw_p2x_ckey(c) desc, job asc) */
 static int ent_cmp(const void* a, const void* b) {
     const p2x_ent* x = (const p2x_ent*)a;
     const p2x_ent* y = (const p2x_ent*)b;
-    if (x->c != y->c) return x->c > y->c ? -1 : 1;
+    const uint64_t kx = sw_p2x_ckey(x->c), ky = sw_p2x_ckey(y->c);
+    if (kx != ky) return kx > ky ? -1 : 1;
     return x->job < y->job ? -1 : (x->job > y->job);
 }
 
@@ -69,16 +71,28 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
     }
 }
 
-/* Bellman–Ford (Jacobi) over rounds 0..T−1 and V = T; *len nodes of a
- * negative cycle into cyc (in predecessor order: cyc[i+1] = pred(cyc[i])),
- * 0 when there is none. */
+/* Bellman–Ford (Jacobi) over rounds 0..T−1 and V = T; after the odd
+ * sweeps and the last the predecessor graph is checked for a cycle (the one reached from the
+ * lowest round whose predecessor walk never ends).  Returns its length and
+ * its nodes from the lowest one in predecessor order (cyc[i+1] =
+ * pred(cyc[i])) when its cost is negative, else 0. */
+#ifdef P2X_DEBUG
+#include <stdio.h>
+static long dbg_it, dbg_bf, dbg_walk;
+#endif
 static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
+#ifdef P2X_DEBUG
+    dbg_bf++;
+#endif
     const int32_t T = X->T;
     double d[SW_TMAX + 1], nd[SW_TMAX + 1];
     int32_t pr[SW_TMAX + 1], np[SW_TMAX + 1];
     for (int32_t x = 0; x <= T; ++x) { d[x] = 0.0; pr[x] = -1; }
     for (int32_t it = 0; it <= T; ++it) {
         int changed = 0;
+#ifdef P2X_DEBUG
+        dbg_it++;
+#endif
         for (int32_t u = 0; u < T; ++u) {
             double best = d[u];
             int32_t bp = pr[u];
@@ -104,13 +118,19 @@ static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
         }
         if (!changed) return 0;
         for (int32_t x = 0; x <= T; ++x) { d[x] = nd[x]; pr[x] = np[x]; }
+        /* checked after the odd sweeps and the last one (after the first
+         * sweep every predecessor is a later round: no cycle can exist) */
+        if (!(it & 1) && it != T) continue;
         /* a cycle of the predecessor graph: T + 1 steps from x still defined */
         for (int32_t x = 0; x <= T; ++x) {
             int32_t y = x;
             for (int32_t s = 0; s <= T && y >= 0; ++s) y = pr[y];
             if (y < 0) continue;
-            int32_t len = 0, v = y;
-            do { cyc[len++] = v; v = pr[v]; } while (v != y);
+            /* the cycle from its lowest node */
+            int32_t lo = y;
+            for (int32_t v = pr[y]; v != y; v = pr[v]) lo = v < lo ? v : lo;
+            int32_t len = 0, v = lo;
+            do { cyc[len++] = v; v = pr[v]; } while (v != lo);
             /* its exact cost, in this order (edges pred(v) → v) */
             double cost = 0.0;
             for (int32_t i = 0; i < len; ++i) {
@@ -159,7 +179,7 @@ static void cancel(p2x_t* X, int32_t F, const int32_t* cyc, int32_t len, int32_t
  */
 int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const int32_t* w,
                      const double* c, uint64_t* m) {
-    if (A <= 0 || T < 2) return 0;
+    if (A <= 0 || T < 2 || A > SW_P2X_AMAX) return 0;
     p2x_t* X = (p2x_t*)calloc(1, sizeof(p2x_t));
     X->T = T;
     X->G = G;
@@ -225,7 +245,7 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
         }
     const double delta = SW_P2X_EPS * twin_detsum(v, A) / (double)T;
     int32_t cyc[SW_TMAX + 1];
-    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)(SW_TMAX + 1) * SW_MAX_WIDTH);
+    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)SW_P2X_MAX_MOVES);
     int32_t ncancel = 0;
     for (int changed = 1; changed && ncancel < SW_P2X_MAX_CANCEL;) {
         changed = 0;
@@ -235,12 +255,22 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                 build_w(X, F, delta);
                 const int32_t len = find_cycle(X, F, cyc);
                 if (len == 0) break;
+                int32_t moves = 0; /* the cycle's job moves */
+                for (int32_t i = 0; i < len; ++i) {
+                    const int32_t u = cyc[i], t = cyc[(i + 1) % len];
+                    if (u < T && t < T) moves += F / X->wc[X->Wk[t * T + u]];
+                }
+                if (moves > SW_P2X_MAX_MOVES) break;
                 cancel(X, F, cyc, len, tmp);
                 ++ncancel;
                 changed = 1;
             }
         }
     }
+#ifdef P2X_DEBUG
+    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld\n", A, X->K, ncancel, dbg_bf, dbg_it);
+    dbg_bf = dbg_it = 0;
+#endif
     /* back to the input order */
     for (int32_t q = 0; q < A; ++q) {
         int32_t lo = 0, hi = A - 1;

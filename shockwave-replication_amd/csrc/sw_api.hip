@@ -22,9 +22,13 @@
 #include "sw_handle.h"
 #include "sw_validate.h"
 
+#define SW_P2X_ARR_BYTES 24 /* sw_p2x_dev.h: exchange workspace bytes per job */
+
 extern "C" size_t sw_plan_kernel_lds_bytes(int one);
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream);
+extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, unsigned char* ws,
+                                    hipStream_t stream);
 
 namespace {
 
@@ -55,6 +59,9 @@ int collect_timing(sw_handle* h) {
         float ms = 0.f;
         SW_HIP(h, hipEventElapsedTime(&ms, h->ev_pool[2 * i], h->ev_pool[2 * i + 1]));
         h->ms_plan += ms;
+        SW_HIP(h, hipEventSynchronize(h->ev_p2x[2 * i + 1]));
+        SW_HIP(h, hipEventElapsedTime(&ms, h->ev_p2x[2 * i], h->ev_p2x[2 * i + 1]));
+        h->ms_p2x += ms;
         h->runs += 1;
     }
     h->ev_used = 0;
@@ -101,8 +108,9 @@ sw_handle* sw_create(const sw_config* cfg) {
         }
     }
     h->ev_pool.assign(2 * kEventPairs, nullptr);
-    for (size_t i = 0; e == hipSuccess && i < h->ev_pool.size(); ++i)
-        e = hipEventCreate(&h->ev_pool[i]);
+    h->ev_p2x.assign(2 * kEventPairs, nullptr);
+    for (size_t i = 0; e == hipSuccess && i < h->ev_pool.size(); ++i) e = hipEventCreate(&h->ev_pool[i]);
+    for (size_t i = 0; e == hipSuccess && i < h->ev_p2x.size(); ++i) e = hipEventCreate(&h->ev_p2x[i]);
     if (e != hipSuccess) {
         g_create_error = std::string("HIP init failed: ") + hipGetErrorString(e);
         sw_destroy(h);
@@ -112,7 +120,7 @@ sw_handle* sw_create(const sw_config* cfg) {
     if (cfg && cfg->max_instances > 0 && cfg->max_total_jobs > 0) {
         size_t J = (size_t)cfg->max_total_jobs, I = (size_t)cfg->max_instances;
         if (h->d_inst.reserve(I) || h->d_out.reserve(I) || h->d_w.reserve(J) ||
-            h->d_F.reserve(J) || h->d_E.reserve(J) || h->d_planned.reserve(J) ||
+            h->d_F.reserve(J) || h->d_E.reserve(J) || h->d_planned.reserve(J) || h->d_masks.reserve(J) ||
             h->d_d.reserve(J) || h->d_R.reserve(J) || h->d_p.reserve(J) ||
             h->d_plan.reserve(J * SW_MAX_ROUNDS)) {
             g_create_error = "device reservation failed";
@@ -133,9 +141,12 @@ void sw_destroy(sw_handle* h) {
     h->d_planned.release(); h->d_d.release(); h->d_R.release(); h->d_p.release();
     h->d_plan.release(); h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
     h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_out.release(); h->d_stamps.release();
+    h->d_masks.release(); h->d_p2ws.release();
     h->h_w.release(); h->h_F.release(); h->h_E.release(); h->h_planned.release();
     h->h_d.release(); h->h_R.release(); h->h_p.release(); h->h_plan.release(); h->h_out.release();
     for (hipEvent_t ev : h->ev_pool)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : h->ev_p2x)
         if (ev) (void)hipEventDestroy(ev);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -173,7 +184,7 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
     if (h->d_inst.reserve(std::max(count, 1)) || h->d_out.reserve(std::max(count, 1)) ||
         h->d_w.reserve(Jz) || h->d_F.reserve(Jz) || h->d_E.reserve(Jz) ||
         h->d_planned.reserve(Jz) || h->d_d.reserve(Jz) || h->d_R.reserve(Jz) ||
-        h->d_p.reserve(Jz) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
+        h->d_p.reserve(Jz) || h->d_masks.reserve(Jz) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS || maxT > 32) {
         const int KT = maxT <= 32 ? 32 : 64;
@@ -182,6 +193,8 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
             h->d_ws_jc.reserve(Jz))
             return fail(h, SW_ERR_HIP, "workspace allocation failed");
     }
+    if (h->d_p2ws.reserve(Jz * SW_P2X_ARR_BYTES))
+        return fail(h, SW_ERR_HIP, "P2 exchange workspace allocation failed");
     if (h->h_w.reserve(Jz) || h->h_F.reserve(Jz) || h->h_E.reserve(Jz) || h->h_d.reserve(Jz) ||
         h->h_R.reserve(Jz) || h->h_p.reserve(Jz) || h->h_planned.reserve(Jz) ||
         h->h_plan.reserve((size_t)std::max<int64_t>(P, 1)) ||
@@ -277,6 +290,7 @@ int sw_batch_run(sw_handle* h) {
     B.p = h->d_p.p;
     B.plan = h->d_plan.p;
     B.planned = h->d_planned.p;
+    B.masks = h->d_masks.p;
     B.out = h->d_out.p;
 #ifdef SW_STAMPS
     B.stamps = h->d_stamps.p;
@@ -298,6 +312,13 @@ int sw_batch_run(sw_handle* h) {
     if (e != hipSuccess) return hip_fail(h, e, "sw_plan_kernel launch");
     if (h->timing) {
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], h->stream));
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], h->stream));
+    }
+    /* the P2 exchange step (sw_p2x_kernel.hip) on the plan kernel's masks */
+    e = sw_launch_p2x(&B, h->maxN, h->maxT, h->d_p2ws.p, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "sw_p2x_kernel launch");
+    if (h->timing) {
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used + 1], h->stream));
         h->ev_used++;
     }
     return SW_OK;
@@ -358,15 +379,16 @@ int sw_set_timing(sw_handle* h, int32_t enable) {
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
     h->timing = enable != 0;
     h->ms_plan = 0.0;
+    h->ms_p2x = 0.0;
     h->runs = 0;
     return SW_OK;
 }
 
-int sw_kernel_times(sw_handle* h, double* ms_rows, double* ms_plan, int32_t* runs) {
+int sw_kernel_times(sw_handle* h, double* ms_p2x, double* ms_plan, int32_t* runs) {
     if (!h) return SW_ERR_INVALID;
     SW_HIP(h, hipSetDevice(h->device));
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
-    if (ms_rows) *ms_rows = 0.0; /* rows are built inside the plan kernel */
+    if (ms_p2x) *ms_p2x = h->ms_p2x;
     if (ms_plan) *ms_plan = h->ms_plan;
     if (runs) *runs = h->runs;
     return SW_OK;

@@ -8,6 +8,8 @@
  *                       inst[i].job_off)
  *   plan bytes          [Σ_i N_i·T_i] row-major per instance ([N_i][T_i])
  *   planned rounds      [Σ_i N_i] int32
+ *   round masks         [Σ_i N_i] u64 (bit t: round t), the plan kernel's
+ *                       final placement, read by the P2 exchange kernel
  *   per-instance out    sw_out_dev
  *   workspace (only for instances with N > SW_LDS_JOBS): per-job state,
  *                       fp32 key rows [job][KT], masks, sort keys.
@@ -17,7 +19,7 @@
 
 #include "sw_arith.h"
 
-#define SW_STAMP_SLOTS 32 /* per-instance u64 slots of the SW_STAMPS diagnostic build */
+#define SW_STAMP_SLOTS 48 /* per-instance u64 slots of the SW_STAMPS diagnostic build (32…47: sw_p2x_kernel) */
 #define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip (2 per thread) */
 
 struct sw_inst_dev {
@@ -61,6 +63,7 @@ struct sw_batch_dev {
     const double* p;
     uint8_t* plan;
     int32_t* planned;
+    uint64_t* masks;
     sw_out_dev* out;
     sw_ws_dev ws;
     uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][16] cycles (8…13: pack round-loop phases) */

@@ -79,6 +79,8 @@ struct sw_handle {
     DevBuf<float> d_ws_keys;
     DevBuf<sw_jobc> d_ws_jc;
     DevBuf<sw_out_dev> d_out;
+    DevBuf<uint64_t> d_masks;     /* final round masks (plan kernel → P2 exchange) */
+    DevBuf<unsigned char> d_p2ws; /* P2 exchange arrays of instances > SW_LDS_JOBS jobs */
     DevBuf<uint64_t> d_stamps; /* SW_STAMPS diagnostic builds */
     /* pinned staging */
     HostBuf<int32_t> h_w, h_F, h_E, h_planned;
@@ -89,7 +91,8 @@ struct sw_handle {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0; /* pairs recorded and not yet collected */
-    double ms_plan = 0.0;
+    std::vector<hipEvent_t> ev_p2x; /* one pair per timed launch of sw_p2x_kernel */
+    double ms_plan = 0.0, ms_p2x = 0.0;
     int32_t runs = 0;
     /* sharded mode (sw_shard.hip) */
     sw_shard_state* shard = nullptr;

@@ -1732,6 +1732,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         }
         p2 = p2 + term;
         B.planned[jo + j] = cnt;
+        B.masks[jo + j] = m; /* for the P2 exchange kernel (sw_p2x_kernel.hip) */
     });
     /* the four emit results in one reduction; its barrier: every mask row
      * is final */

@@ -40,10 +40,22 @@
 
 #include "sw_arith.h"
 
-#define SW_P2X_EPS 1e-4        /* δ = ε·P2₀/T per edge                          */
+#ifdef SW_P2X_EPS_OVERRIDE /* experiments only */
+#define SW_P2X_EPS SW_P2X_EPS_OVERRIDE
+#else
+#define SW_P2X_EPS 2e-4        /* δ = ε·P2₀/T per edge                          */
+#endif
 #define SW_P2X_MAX_CANCEL 256  /* cancels per solve                              */
 #define SW_P2X_KMAX 8          /* width classes handled (more: the step is skipped) */
 #define SW_P2X_NONE 1.0e300    /* "no edge" cost                                 */
+#define SW_P2X_AMAX 4096       /* active jobs handled (more: the step is skipped) */
+#define SW_P2X_MAX_MOVES 1024  /* job moves one cycle may make (more: the cycle is
+                                  not cancelled and the load size F is done)     */
+
+/* Rank order inside a class: this key descending (c = p/n ≥ 0 without its
+ * 3 lowest mantissa bits, so it fits beside a class index in one word), then
+ * job ascending. */
+SW_HD uint64_t sw_p2x_ckey(double c) { return sw_bits(c) >> 3; }
 
 /* The ranks the edge t → u moves in one class: X = Bt & ~Bu over the class's
  * rank bitset (nw words; rank r = bit r % 64 of word r / 64, ranks in
@@ -91,19 +103,35 @@ SW_HD int32_t sw_p2x_next(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, in
     return 64 * i + __builtin_ctzll(x);
 }
 
-/* Cost of the class's edge: Σ c over the selected ranks (ascending) times
- * (u − t); SW_P2X_NONE when the class has no such edge.  c is the class's
- * c array indexed by rank. */
+/* Cost of the class's edge: the Σ of c over the selected ranks, summed in
+ * selection order (ascending ranks when u < t, descending when u > t),
+ * times (u − t); SW_P2X_NONE when X has fewer than q ranks.  c is the
+ * class's c array indexed by rank.  One pass over the words. */
 SW_HD double sw_p2x_cost(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t q, int32_t t,
                          int32_t u, const double* c) {
-    int32_t r = sw_p2x_start(Bt, Bu, nw, q, u < t);
-    if (r < 0) return SW_P2X_NONE;
     double s = 0.0;
-    for (int32_t g = 0; g < q; ++g) {
-        s = s + c[r];
-        if (g + 1 < q) r = sw_p2x_next(Bt, Bu, nw, r + 1);
+    int32_t got = 0;
+    if (u < t) {
+        for (int32_t i = 0; i < nw && got < q; ++i) {
+            uint64_t x = Bt[i] & ~Bu[i];
+            while (x && got < q) {
+                s = s + c[64 * i + __builtin_ctzll(x)];
+                x &= x - 1;
+                ++got;
+            }
+        }
+    } else {
+        for (int32_t i = nw - 1; i >= 0 && got < q; --i) {
+            uint64_t x = Bt[i] & ~Bu[i];
+            while (x && got < q) {
+                const int32_t b = 63 - __builtin_clzll(x);
+                s = s + c[64 * i + b];
+                x &= ~(1ull << b);
+                ++got;
+            }
+        }
     }
-    return s * (double)(u - t);
+    return got == q ? s * (double)(u - t) : SW_P2X_NONE;
 }
 
 #endif /* SW_P2X_H */

@@ -1,0 +1,557 @@
+/*
+ * sw_p2x_dev.h — the P2 exchange step as a block function (sw_p2x.h;
+ * DESIGN.md §3.6), bit-identical to the sequential specification
+ * oracle/p2x_twin.c.  Used by the batch kernel (sw_p2x_kernel.hip) and by the
+ * sharded engine on its gathered placement (sw_shard.hip).
+ *
+ * Mapping.  Active jobs are ranked inside their width class by (c desc, job
+ * asc) with an all-pairs count (LDS tiles), and each class's membership of
+ * each round becomes a rank bitset in LDS, so the move an edge t → u makes is
+ * a few 64-bit and-not / ctz / clz word operations.  Edge costs W[t][u] are
+ * built by all threads, one (t, u) pair per thread, once per load size F and
+ * afterwards only in the rows and columns of the rounds a cancelled cycle
+ * touched (the other entries cannot change).  Wave 0 runs Bellman–Ford with
+ * one round per lane: the relaxations read the other lanes' distances with
+ * readlane (the round index is wave-uniform), the free-capacity node V is a
+ * wave-uniform scalar, and the predecessor check uses pointer doubling
+ * (7 shuffles reach 128 ≥ T + 1 steps).  A cycle's moves are applied with LDS
+ * atomics.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/shockwave_amd.h"
+#include "sw_arith.h"
+#include "sw_block.h"
+#include "sw_device.h"
+#include "sw_p2x.h"
+
+/* per-active-job arrays, index a = active jobs in job order (LDS on the
+ * on-chip batch path, HBM workspace otherwise) */
+struct sw_p2x_arrays {
+    int32_t* cw;  /* width                       */
+    int32_t* cj;  /* job id                      */
+    double* cc;   /* c = p / n                   */
+    uint64_t* cm; /* round mask (improved here)  */
+};
+#define SW_P2X_ARR_BYTES 24 /* bytes per job of sw_p2x_arrays */
+
+/* fixed LDS part */
+struct sw_p2x_lds {
+    sw_xchg X;
+    int32_t wc[SW_P2X_KMAX], M[SW_P2X_KMAX], off[SW_P2X_KMAX + 1], nw[SW_P2X_KMAX],
+        boff[SW_P2X_KMAX];
+    int32_t K, len, nrec, pad;
+    uint64_t touched; /* rounds the last cancelled cycle moved jobs in or out of */
+    uint32_t wmap[8]; /* widths present (256 bits) */
+    int32_t room[SW_TMAX];
+    int32_t pr[SW_TMAX + 1];
+    int32_t cyc[SW_TMAX + 2];
+    double delta;
+    /* block-wide Bellman–Ford: distances and predecessors (V at index T),
+     * the four relaxing waves' partial minima, the loop's exit flag */
+    double bd[SW_TMAX + 1];
+    int32_t bp[SW_TMAX + 1];
+    double pv[4][64];
+    int32_t pt[4][64];
+    int32_t bfdone;
+    int32_t fq[SW_P2X_KMAX]; /* F / w_k for the current load size (0: w_k ∤ F) */
+};
+
+/* LDS the variable part needs for up to maxA active jobs and T rounds:
+ * position order and c by position, then the larger of (rank bitsets, W,
+ * Wk, move records) and the rank sort's scratch (16 B per entry of the next
+ * power of two) */
+__host__ __device__ inline size_t sw_p2x_var_bytes(int maxA, int T) {
+    const size_t a = (size_t)(maxA < SW_P2X_AMAX ? maxA : SW_P2X_AMAX);
+    const size_t words = (size_t)T * ((a + 63) / 64 + SW_P2X_KMAX);
+    size_t np = 1;
+    while (np < a) np <<= 1;
+    const size_t work = words * 8 + (size_t)T * T * 8 + (((size_t)T * T + 15) & ~(size_t)15) +
+                        (size_t)SW_P2X_MAX_MOVES * 4;
+    return a * 8 + ((a * 4 + 15) & ~(size_t)15) + (work > 16 * np ? work : 16 * np);
+}
+
+static __device__ __forceinline__ int p2x_class(const sw_p2x_lds* L, int32_t w) {
+    int k = 0;
+    while (k < L->K - 1 && L->wc[k] != w) ++k;
+    return k;
+}
+
+/* Bellman–Ford of oracle/p2x_twin.c find_cycle, block-wide: each sweep,
+ * waves 0–3 relax one quarter of the source rounds each (lane u = target
+ * round u: the smallest d[t] + W[t][u] of the quarter and its first t, read
+ * against the distances in LDS), then wave 0 combines the quarters in round
+ * order (strict <: the sequential scan's answer), adds V (a wave-uniform
+ * scalar), publishes the new distances and, after the odd sweeps and the
+ * last, checks the predecessor graph for a cycle by pointer doubling
+ * (7 shuffles reach 128 ≥ T + 1 steps).  Leaves the cycle in L->cyc / L->len
+ * (0: none).  All threads call it. */
+static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const double* W, int T, int F,
+                                                      uint64_t* sp = nullptr) {
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    (void)sp;
+#ifdef SW_STAMPS
+    uint64_t bt_ = __builtin_amdgcn_s_memtime();
+#define BF_STAMP(k)                                                   \
+    do {                                                              \
+        if (tid == 0 && sp) {                                         \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();       \
+            sp[k] += now_ - bt_;                                      \
+            bt_ = now_;                                               \
+        }                                                             \
+    } while (0)
+#else
+#define BF_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+    const bool act = lane < T;
+    if (tid <= T) {
+        L->bd[tid] = 0.0;
+        L->bp[tid] = -1;
+    }
+    if (tid == 0) L->bfdone = 0;
+    const bool roomok = wv == 0 && act && L->room[lane] >= F;
+    const bool anyroom = __ballot(roomok) != 0; /* else V has no in-edge: it never changes */
+    const int nq = (T + 3) >> 2;
+    __syncthreads();
+    for (int it = 0; it <= T; ++it) {
+#ifdef SW_STAMPS
+        if (tid == 0 && sp) sp[7] += 1;
+#endif
+        BF_STAMP(10);
+        if (wv < 4) {
+            /* W[t][t] and missing edges are SW_P2X_NONE and every distance is
+             * ≤ 0, so they never win: no per-edge tests */
+            const int ul = act ? lane : 0;
+            const int t0 = wv * nq, t1 = min(T, t0 + nq);
+            double cb = SW_P2X_NONE;
+            int ct = 0;
+            for (int t = t0; t < t1; ++t) {
+                const double v = L->bd[t] + W[t * T + ul];
+                const bool take = v < cb;
+                cb = take ? v : cb;
+                ct = take ? t : ct;
+            }
+            L->pv[wv][lane] = cb;
+            L->pt[wv][lane] = ct;
+        }
+        __syncthreads();
+        BF_STAMP(9);
+        if (wv == 0) {
+            double d = act ? L->bd[lane] : 0.0;
+            int pr = act ? L->bp[lane] : -1;
+            const double dV = L->bd[T];
+            int prV = L->bp[T];
+            double cb = L->pv[0][lane];
+            int ct = L->pt[0][lane];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                const double v = L->pv[q][lane];
+                const bool take = q * nq < T && v < cb;
+                cb = take ? v : cb;
+                ct = take ? L->pt[q][lane] : ct;
+            }
+            double best = d;
+            int bpr = pr;
+            if (cb < best) {
+                best = cb;
+                bpr = ct;
+            }
+            if (act && dV < best) {
+                best = dV;
+                bpr = T;
+            }
+            /* V: the smallest d over rounds with F free GPUs, lowest round on ties */
+            bool vbetter = false;
+            double m = dV;
+            uint64_t at = 0;
+            if (anyroom) {
+                m = wave_min(roomok ? d : SW_P2X_NONE);
+                at = __ballot(roomok && d == m);
+                vbetter = m < dV;
+            }
+            const bool changed = __ballot(act && best < d) != 0 || vbetter;
+            int done = 0;
+            if (!changed) {
+                done = 1;
+                if (lane == 0) L->len = 0;
+            } else {
+                d = best;
+                pr = bpr;
+                if (vbetter) prV = (int)__builtin_ctzll(at);
+                if (act) {
+                    L->bd[lane] = d;
+                    L->bp[lane] = pr;
+                }
+                if (lane == 0 && vbetter) {
+                    L->bd[T] = m;
+                    L->bp[T] = prV;
+                }
+                /* after the odd sweeps and the last (after the first, every
+                 * predecessor is a later round: no cycle can exist yet) */
+                if ((it & 1) || it == T) {
+                    int y = act ? pr : -1, yV = prV;
+                    for (int s2 = 0; s2 < 7; ++s2) {
+                        const int g = __shfl(y, (y >= 0 && y < T) ? y : 0, 64);
+                        const int gV = (yV >= 0 && yV < T) ? __shfl(y, yV, 64) : (yV == T ? yV : -1);
+                        y = y < 0 ? -1 : (y == T ? yV : g);
+                        yV = gV;
+                    }
+                    const uint64_t cbits = __ballot(act && y >= 0);
+                    if (cbits) {
+                        done = 1;
+                        const int y0 = __shfl(y, (int)__builtin_ctzll(cbits), 64);
+                        if (act) L->pr[lane] = pr;
+                        if (lane == 0) L->pr[T] = prV;
+                        wave_sync();
+                        if (lane == 0) {
+                            int lo = y0;
+                            for (int v = L->pr[y0]; v != y0; v = L->pr[v]) lo = v < lo ? v : lo;
+                            int len = 0, v = lo;
+                            do {
+                                L->cyc[len++] = v;
+                                v = L->pr[v];
+                            } while (v != lo && len <= T + 1);
+                            double cost = 0.0;
+                            for (int i = 0; i < len; ++i) {
+                                const int u = L->cyc[i], t = L->pr[u];
+                                if (u < T && t < T) cost = cost + W[t * T + u];
+                            }
+                            L->len = cost < 0.0 ? len : 0;
+                        }
+                    }
+                }
+                if (!done && it == T && lane == 0) L->len = 0;
+            }
+            if (lane == 0) L->bfdone = done;
+        }
+        __syncthreads();
+        if (L->bfdone) break;
+    }
+#undef BF_STAMP
+}
+
+/* sw_p2x_cost (sw_p2x.h) for classes of at most 256 jobs and q ≤ 8: the
+ * and-not words are loaded once into registers, the selected ranks found
+ * with register-only bit scans, then their c values read together and summed
+ * in selection order (the same sum).  Other cases take sw_p2x_cost. */
+static __device__ __forceinline__ uint64_t p2x_sel4(const uint64_t (&xw)[4], int i) {
+    return i == 0 ? xw[0] : i == 1 ? xw[1] : i == 2 ? xw[2] : xw[3];
+}
+static __device__ __forceinline__ double p2x_cost_dev(const uint64_t* Bt, const uint64_t* Bu, int nw, int q,
+                                                      int t, int u, const double* c) {
+    if (q > 8 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, q, t, u, c);
+    uint64_t xw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[i] = i < nw ? (Bt[i] & ~Bu[i]) : 0ull;
+    const bool lo = u < t;
+    int wi = lo ? 0 : nw - 1;
+    uint64_t x = p2x_sel4(xw, wi);
+    int rk[8];
+    int got = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        while (x == 0ull && (lo ? wi < nw - 1 : wi > 0)) {
+            wi += lo ? 1 : -1;
+            x = p2x_sel4(xw, wi);
+        }
+        const bool has = x != 0ull && g < q;
+        const int b = lo ? __builtin_ctzll(x) : 63 - __builtin_clzll(x);
+        rk[g] = 64 * wi + b;
+        x = has ? (lo ? x & (x - 1) : x & ~(1ull << b)) : x;
+        got += has;
+    }
+    if (got < q) return SW_P2X_NONE;
+    double cv[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) cv[g] = g < q ? c[rk[g]] : 0.0;
+    double sum = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+        if (g < q) sum = sum + cv[g];
+    return sum * (double)(u - t);
+}
+
+/* W entries for load size F: every entry (all = true) or those in a row or
+ * column of L->touched.  L->fq[k] = F / w_k for the classes that can carry F
+ * (w_k | F), 0 for the others: set once per load size, so the per-entry loop
+ * has no integer divisions. */
+template <int NT>
+static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const uint64_t* B, const double* pc,
+                                                   double* W, int8_t* Wk, int T, double delta, bool all) {
+    const uint64_t tm = L->touched;
+    const int K = L->K;
+    for (int e = threadIdx.x; e < T * T; e += NT) {
+        const int t = e / T, u = e - t * T;
+        if (!all && !(((tm >> t) | (tm >> u)) & 1ull)) continue;
+        double best = SW_P2X_NONE;
+        int bk = -1;
+        if (t != u) {
+#pragma unroll 1
+            for (int k = 0; k < K; ++k) {
+                const int q = L->fq[k];
+                if (q == 0) continue;
+                const int nw = L->nw[k];
+                const uint64_t* Bk = B + L->boff[k];
+#ifdef P2X_EXPERIMENT_TRIVIAL_COST
+                const double cost = (double)(u - t) * pc[L->off[k]] + (double)(Bk[t * nw] & 7);
+#else
+                const double cost = p2x_cost_dev(Bk + t * nw, Bk + u * nw, nw, q, t, u, pc + L->off[k]);
+#endif
+                if (cost < best) {
+                    best = cost;
+                    bk = k;
+                }
+            }
+        }
+        W[e] = bk >= 0 ? best + delta : SW_P2X_NONE;
+        Wk[e] = (int8_t)bk;
+    }
+}
+
+/* diagnostic builds (SW_STAMPS): thread 0 adds cycles to sp[k]: 0 classes,
+ * 1 ranks, 2 bitsets and δ, 3 edge builds, 4 Bellman–Ford, 5 selecting a
+ * cycle's moves, 6 applying them; counts: 7 Bellman–Ford sweeps, 8 edge
+ * builds; inside Bellman–Ford: 9 relaxations, 10 predecessor walks */
+#ifdef SW_STAMPS
+#define P2X_STAMP(k)                                                 \
+    do {                                                             \
+        if (threadIdx.x == 0 && sp) {                                \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+            sp[k] += now_ - sp_t_;                                   \
+            sp_t_ = now_;                                            \
+        }                                                            \
+    } while (0)
+#else
+#define P2X_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
+template <int NW>
+__device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, unsigned char* var,
+                                            const sw_p2x_arrays& X, int A, int T, int G,
+                                            uint64_t* sp = nullptr) {
+    constexpr int NT = NW * 64;
+    const int tid = threadIdx.x;
+    (void)sp;
+#ifdef SW_STAMPS
+    uint64_t sp_t_ = __builtin_amdgcn_s_memtime();
+#endif
+    if (A <= 0 || T < 2 || A > SW_P2X_AMAX) return 0;
+    /* ---- width classes (ascending) ---- */
+    if (tid < 8) L->wmap[tid] = 0u;
+    __syncthreads();
+    for (int a = tid; a < A; a += NT) atomicOr(&L->wmap[X.cw[a] >> 5], 1u << (X.cw[a] & 31));
+    __syncthreads();
+    if (tid == 0) {
+        int K = 0;
+        for (int i = 0; i < 8; ++i) K += __builtin_popcount(L->wmap[i]);
+        if (K > SW_P2X_KMAX) {
+            L->K = -1;
+        } else {
+            K = 0;
+            for (int i = 0; i < 8; ++i)
+                for (uint32_t b = L->wmap[i]; b; b &= b - 1) L->wc[K++] = 32 * i + __builtin_ctz(b);
+            L->K = K;
+            for (int k = 0; k < K; ++k) L->M[k] = 0;
+        }
+    }
+    __syncthreads();
+    const int K = L->K;
+    if (K < 0) return 0;
+    for (int a = tid; a < A; a += NT) atomicAdd(&L->M[p2x_class(L, X.cw[a])], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int o = 0, b = 0;
+        for (int k = 0; k < K; ++k) {
+            L->off[k] = o;
+            L->nw[k] = (L->M[k] + 63) / 64;
+            L->boff[k] = b;
+            o += L->M[k];
+            b += L->nw[k] * T;
+        }
+        L->off[K] = o;
+    }
+    P2X_STAMP(0);
+    /* LDS carve-up of var */
+    double* pc = reinterpret_cast<double*>(var);                      /* c by position        */
+    int32_t* ord = reinterpret_cast<int32_t*>(var + (size_t)A * 8);  /* position → a         */
+    unsigned char* vb = var + (size_t)A * 8 + (((size_t)A * 4 + 15) & ~(size_t)15);
+    __syncthreads();
+    const int nwords = L->boff[K - 1] + L->nw[K - 1] * T;
+    uint64_t* B = reinterpret_cast<uint64_t*>(vb);
+    double* W = reinterpret_cast<double*>(vb + (size_t)nwords * 8);
+    int8_t* Wk = reinterpret_cast<int8_t*>(W + T * T);
+    int32_t* rec = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned char*>(Wk) + ((T * T + 15) & ~15));
+    /* ---- positions: (class asc, sw_p2x_ckey(c) desc, job asc) by a bitonic
+     *      sort in LDS over the next power of two (the bitset / W area is
+     *      free until the first build) ---- */
+    {
+        int np = 1;
+        while (np < A) np <<= 1;
+        uint64_t* k1 = reinterpret_cast<uint64_t*>(vb);
+        uint32_t* k2 = reinterpret_cast<uint32_t*>(k1 + np); /* job */
+        uint32_t* ka = k2 + np;                              /* a   */
+        for (int i = tid; i < np; i += NT) {
+            if (i < A) {
+                const uint64_t ck = sw_p2x_ckey(X.cc[i]);
+                k1[i] = ((uint64_t)p2x_class(L, X.cw[i]) << 61) | (~ck & ((1ull << 61) - 1));
+                k2[i] = (uint32_t)X.cj[i];
+                ka[i] = (uint32_t)i;
+            } else {
+                k1[i] = ~0ull;
+                k2[i] = 0xFFFFFFFFu;
+                ka[i] = 0u;
+            }
+        }
+        __syncthreads();
+        for (int k = 2; k <= np; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int x = tid; x < (np >> 1); x += NT) {
+                    const int i = 2 * x - (x & (j - 1)), l = i + j;
+                    const uint64_t a1 = k1[i], b1 = k1[l];
+                    const uint32_t a2 = k2[i], b2 = k2[l];
+                    const bool gt = a1 > b1 || (a1 == b1 && a2 > b2);
+                    if (((i & k) == 0) == gt) { /* ascending blocks where bit k of i is clear */
+                        k1[i] = b1; k1[l] = a1;
+                        k2[i] = b2; k2[l] = a2;
+                        const uint32_t t = ka[i]; ka[i] = ka[l]; ka[l] = t;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int p = tid; p < A; p += NT) {
+            const int a = (int)ka[p];
+            ord[p] = a;
+            pc[p] = X.cc[a];
+        }
+        __syncthreads(); /* the sort scratch is read before the bitsets clear it */
+    }
+    P2X_STAMP(1);
+    /* ---- rank bitsets, free capacity, δ ---- */
+    for (int i = tid; i < nwords; i += NT) B[i] = 0ull;
+    if (tid < T) L->room[tid] = G;
+    __syncthreads();
+    for (int p = tid; p < A; p += NT) {
+        int k = 0;
+        while (p >= L->off[k + 1]) ++k;
+        const int r = p - L->off[k];
+        for (uint64_t m = X.cm[ord[p]]; m; m &= m - 1) {
+            const int t = __builtin_ctzll(m);
+            atomicOr((unsigned long long*)&B[L->boff[k] + t * L->nw[k] + (r >> 6)], 1ull << (r & 63));
+            atomicAdd(&L->room[t], -L->wc[k]);
+        }
+    }
+    {
+        /* sw_detsum over positions: lane l sums [l·q, (l+1)·q) left to right */
+        const int q = (A + SW_DET_LANES - 1) / SW_DET_LANES;
+        static_assert(NT == SW_DET_LANES, "one thread per deterministic-sum lane");
+        double acc = 0.0;
+        for (int p = tid * q; p < A && p < (tid + 1) * q; ++p) {
+            int64_t S = 0;
+            for (uint64_t x = X.cm[ord[p]]; x; x &= x - 1) S += __builtin_ctzll(x);
+            acc = acc + pc[p] * (double)S;
+        }
+        const double P0 = blk.detsum(acc); /* its barrier publishes B, room */
+        if (tid == 0) L->delta = SW_P2X_EPS * P0 / (double)T;
+    }
+    __syncthreads();
+    const double delta = L->delta;
+    P2X_STAMP(2);
+    /* ---- cancelling ---- */
+    int ncancel = 0;
+    for (bool changed = true; changed && ncancel < SW_P2X_MAX_CANCEL;) {
+        changed = false;
+        for (int ki = 0; ki < K && ncancel < SW_P2X_MAX_CANCEL; ++ki) {
+            const int F = L->wc[ki];
+            if (tid < SW_P2X_KMAX) {
+                const int wk = tid < K ? L->wc[tid] : 0;
+                L->fq[tid] = (wk > 0 && wk <= F && F % wk == 0) ? F / wk : 0;
+            }
+            __syncthreads();
+            bool all = true;
+            while (ncancel < SW_P2X_MAX_CANCEL) {
+                p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
+                __syncthreads();
+                P2X_STAMP(3);
+#ifdef SW_STAMPS
+                if (threadIdx.x == 0 && sp) sp[8] += 1;
+#endif
+                p2x_find_cycle(L, W, T, F, sp);
+                P2X_STAMP(4);
+                const int len = L->len;
+                if (len == 0) break;
+                /* the cycle's moves, all selected before any is applied: wave 0,
+                 * one lane per edge (edge i: pred(cyc[i]) → cyc[i]) */
+                if (wave_id() == 0) {
+                    const int lane = lane_id();
+                    int moves = 0;
+                    uint64_t tm = 0;
+                    for (int b0 = 0; b0 < len; b0 += 64) {
+                        const int i = b0 + lane;
+                        const int u = i < len ? L->cyc[i] : T, t = i < len ? L->cyc[(i + 1) % len] : T;
+                        const bool real = u < T && t < T;
+                        const int q = real ? F / L->wc[Wk[t * T + u]] : 0;
+                        moves += wave_sum_i32(q);
+                    }
+                    int n0 = 0;
+                    for (int b0 = 0; b0 < len; b0 += 64) {
+                        const int i = b0 + lane;
+                        const int u = i < len ? L->cyc[i] : T, t = i < len ? L->cyc[(i + 1) % len] : T;
+                        const bool real = u < T && t < T;
+                        const int k = real ? Wk[t * T + u] : 0;
+                        const int q = real ? F / L->wc[k] : 0;
+                        const int incl = wave_incscan_i32(q);
+                        if (real) tm |= (1ull << t) | (1ull << u);
+                        if (real && moves <= SW_P2X_MAX_MOVES) {
+                            const uint64_t* Bt = B + L->boff[k] + t * L->nw[k];
+                            const uint64_t* Bu = B + L->boff[k] + u * L->nw[k];
+                            int r = sw_p2x_start(Bt, Bu, L->nw[k], q, u < t);
+                            int n = n0 + incl - q;
+                            for (int g = 0; g < q; ++g) {
+                                rec[n++] = (k << 29) | (t << 23) | (u << 17) | r;
+                                if (g + 1 < q) r = sw_p2x_next(Bt, Bu, L->nw[k], r + 1);
+                            }
+                        }
+                        n0 += __shfl(incl, 63, 64);
+                    }
+                    /* every lane's touched rounds */
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        const uint64_t v = (uint64_t)__shfl_xor((long long)tm, o, 64);
+                        tm |= v;
+                    }
+                    if (lane == 0) {
+                        L->nrec = moves <= SW_P2X_MAX_MOVES ? n0 : -1;
+                        L->touched = tm;
+                    }
+                }
+                __syncthreads();
+                P2X_STAMP(5);
+                const int nrec = L->nrec;
+                if (nrec < 0) break;
+                for (int i = tid; i < nrec; i += NT) {
+                    const int32_t v = rec[i];
+                    const int k = (v >> 29) & 7, t = (v >> 23) & 63, u = (v >> 17) & 63, r = v & 0x1FFFF;
+                    uint64_t* Bk = B + L->boff[k];
+                    const uint64_t bit = 1ull << (r & 63);
+                    atomicAnd((unsigned long long*)&Bk[t * L->nw[k] + (r >> 6)], ~bit);
+                    atomicOr((unsigned long long*)&Bk[u * L->nw[k] + (r >> 6)], bit);
+                    atomicXor((unsigned long long*)&X.cm[ord[L->off[k] + r]], (1ull << t) | (1ull << u));
+                    atomicAdd(&L->room[t], L->wc[k]);
+                    atomicAdd(&L->room[u], -L->wc[k]);
+                }
+                __syncthreads();
+                P2X_STAMP(6);
+                ++ncancel;
+                changed = true;
+                all = false;
+            }
+        }
+    }
+    return ncancel;
+}

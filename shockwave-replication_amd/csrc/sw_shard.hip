@@ -59,6 +59,8 @@
 #include "sw_block.h"
 #include "sw_device.h"
 #include "sw_handle.h"
+#include "sw_p2x.h"
+#include "sw_p2x_dev.h"
 #include "sw_pack.h"
 #include "sw_shard_ctl.h"
 #include "sw_validate.h"
@@ -823,6 +825,69 @@ __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_en
     pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
 }
 
+/* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
+
+/* one gathered entry per job (the pack's gather buffer, reused) */
+struct p2x_ent {
+    uint64_t m; /* round mask of the P2 placement */
+    double p;   /* priority                       */
+    int32_t n, w;
+};
+static_assert(sizeof(p2x_ent) == sizeof(sw_pack_ent), "p2x entries reuse the pack's gather buffer");
+
+__global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, const int32_t* n,
+                                                 p2x_ent* out) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.P) return;
+    p2x_ent e;
+    e.m = 0; e.p = 0.0; e.n = 0; e.w = 0;
+    if (i < S.NL) {
+        e.m = y[i]; e.p = S.p[i]; e.n = n[i]; e.w = S.jc[i].w;
+    }
+    out[i] = e;
+}
+
+/* The step on the M gathered entries (entry j = job j), one workgroup, the
+ * same on every rank; writes this rank's rows of ydst and the number of
+ * cycles cancelled into red[0]. */
+__global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all, int64_t M,
+                                                  unsigned char* ws, uint64_t* ydst) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    sw_p2x_lds* L = reinterpret_cast<sw_p2x_lds*>(smem);
+    unsigned char* var = smem + ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15);
+    sw_blk blk;
+    blk.X = &L->X;
+    blk.par = 0;
+    sw_p2x_arrays X;
+    X.cc = reinterpret_cast<double*>(ws);
+    X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
+    X.cw = reinterpret_cast<int32_t*>(X.cm + M);
+    X.cj = X.cw + M;
+    const int64_t q = (M + SW_BLOCK - 1) / SW_BLOCK;
+    const int64_t j0 = (int64_t)threadIdx.x * q, j1 = j0 + q < M ? j0 + q : M;
+    int act = 0;
+    for (int64_t j = j0; j < j1; ++j) act += all[j].n > 0;
+    int A;
+    int a = blk.exscan(act, A);
+    for (int64_t j = j0; j < j1; ++j) {
+        const p2x_ent e = all[j];
+        if (e.n <= 0) continue;
+        X.cw[a] = e.w;
+        X.cj[a] = (int32_t)j;
+        X.cc[a] = e.p / (double)e.n;
+        X.cm[a] = e.m;
+        ++a;
+    }
+    __syncthreads();
+    const int nc = sw_p2x_block<SW_WAVES>(blk, L, var, X, A, S.T, S.G);
+    if (nc > 0)
+        for (int i = threadIdx.x; i < A; i += SW_BLOCK) {
+            const int64_t j = X.cj[i];
+            if (j >= S.off && j < S.off + S.NL) ydst[j - S.off] = X.cm[i];
+        }
+    if (threadIdx.x == 0) S.red[0] = nc;
+}
+
 /* Step results to the host without a stream synchronisation: the words are
  * stored into fine-grained pinned host memory, then a sequence number is
  * released at system scope; the host spins on it (sw_shard_state::publish).
@@ -1016,6 +1081,7 @@ struct sw_shard_state {
     DevBuf<uint8_t> plan;
     DevBuf<long long> red, tieblk;
     DevBuf<sw_pack_ent> pall;
+    DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry) */
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
@@ -1551,6 +1617,28 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc
     return SW_OK;
 }
 
+/* twin: e_p2x (oracle/shard_twin.c) — gather the P2 placement, run the
+ * exchange step replicated, keep this rank's rows */
+int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    const int64_t M = S->P * S->world;
+    if (S->p2ws.reserve((size_t)M * SW_P2X_ARR_BYTES)) return host_fail(S, "P2 exchange workspace");
+    p2x_ent* mine = reinterpret_cast<p2x_ent*>(S->pall.p + (size_t)S->rank * S->P);
+    LAUNCH(S, k_p2x_ent, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, S->y[ysrc].p, S->arr[nsrc].p, mine);
+    const void* gv = nullptr;
+    SH_TRY(coll_gather(S, mine, S->pall.p, (size_t)S->P * sizeof(p2x_ent), nullptr, &gv));
+    SH_TRY(zero_red(S, 1));
+    const int maxA = (int)std::min<int64_t>(M, SW_P2X_AMAX);
+    const size_t lds = ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15) + sw_p2x_var_bytes(maxA, S->T);
+    LAUNCH(S, k_p2x, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, (const p2x_ent*)gv, M, S->p2ws.p,
+           S->y[ysrc].p);
+    uint64_t nc = 0;
+    SH_TRY(coll_reduce(S, S->dv.red, 1, 1, &nc)); /* every rank computed the same count */
+    *cancels = (int32_t)nc;
+    return SW_OK;
+}
+
 /* Reserve the per-solve buffers and upload this rank's jobs. */
 int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, bool dev,
             const sw_result* res) {
@@ -1654,7 +1742,7 @@ void sw_shard_release(sw_handle* h) {
     S->tie.release(); S->tieblk.release(); S->xa.release();
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
-    S->plan.release(); S->red.release(); S->pall.release(); S->hx.release();
+    S->plan.release(); S->red.release(); S->pall.release(); S->p2ws.release(); S->hx.release();
     if (S->pub) (void)hipHostFree(S->pub);
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
@@ -1912,6 +2000,7 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.pack = op_pack;
     ops.class_caps = op_class_caps;
     ops.pack_class = op_pack_class;
+    ops.p2x = op_p2x;
     ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,

@@ -12,7 +12,7 @@ import sys
 
 import numpy as np
 
-SLOTS = 32  # SW_STAMP_SLOTS (csrc/sw_device.h)
+SLOTS = 48  # SW_STAMP_SLOTS (csrc/sw_device.h)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shockwave-replication_amd"))
@@ -59,6 +59,12 @@ def main():
         lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
         print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)),
               f"| price probes {st_all[:, 23].mean():.1f}, M_lo passes {st_all[:, 24].mean():.1f}")
+        px = st_all[:, 32:43]
+        pn = ["classes", "ranks", "bitsets", "edges", "bellman_ford", "select", "apply", "bf_iters",
+              "builds", "bf_relax", "bf_walks"]
+        print("   P2 exchange kernel (sw_p2x_kernel):", " ".join(
+            f"{n} {px[:, i].mean():.0f}" for i, n in enumerate(pn)),
+            f"| total {px[:, :7].sum(axis=1).mean():.0f}")
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
             for r, row, prow in list(zip(res, st, pk))[:24]:
                 print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row), "|",
