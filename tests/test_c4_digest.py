@@ -13,6 +13,10 @@ import sw_synth as ss
 
 GOLD = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
                                    "c4_digest.json")))
+# The LP relaxation of the reference P1 (shockwave.py:330-382, binaries relaxed
+# to [0, 1]) on the same instance, solved once by HiGHS
+# (tests/golden/make_c4_lp.py): an upper bound on every integer plan's J.
+LP = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_lp.json")))
 
 
 def c4():
@@ -25,11 +29,32 @@ def digest(plan, counts):
             hashlib.sha256(np.ascontiguousarray(counts, dtype=np.int32).tobytes()).hexdigest()[:32])
 
 
+def inputs_sha(a):
+    h = hashlib.sha256()
+    for arr in (a.w, a.d, a.F, a.E, a.R, a.p):
+        h.update(np.ascontiguousarray(arr).tobytes())
+    return h.hexdigest()[:32]
+
+
+def check_lp_bound(J):
+    """(LP − J) / |J| ≤ 1e-3: the LP relaxation certifies the C4 objective to
+    the north star's tolerance (and J never exceeds the bound)."""
+    assert LP["lp_status"] == "optimal"
+    gap = (LP["lp_bound"] - J) / abs(J)
+    assert -1e-9 <= gap <= 1e-3, (J, LP["lp_bound"], gap)
+
+
 def test_c4_digest_is_the_twin_solve(twin):
     a = c4()
     r = twin.solve(a)
     assert digest(r["plan"], r["planned_rounds"]) == (GOLD["plan_sha"], GOLD["counts_sha"])
     assert float(r["objective"]).hex() == GOLD["objective_hex"]
+
+
+def test_c4_objective_within_lp_bound(twin):
+    a = c4()
+    assert inputs_sha(a) == LP["inputs_sha"], "C4 inputs changed: regenerate tests/golden/c4_lp.json"
+    check_lp_bound(twin.solve(a)["objective"])
 
 
 @pytest.mark.gpu
@@ -43,3 +68,4 @@ def test_gpu_rccl_world1_reproduces_c4_digest():
     s.close()
     assert digest(r["plan"], r["planned_rounds"]) == (GOLD["plan_sha"], GOLD["counts_sha"])
     assert float(r["objective"]).hex() == GOLD["objective_hex"]
+    check_lp_bound(r["objective"])
