@@ -59,7 +59,7 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
             int32_t bk = -1;
             if (u != t) {
                 for (int32_t k = 0; k < X->K; ++k) {
-                    if (X->wc[k] > F || F % X->wc[k] != 0) continue;
+                    if (X->wc[k] > F || F % X->wc[k] != 0 || F / X->wc[k] > SW_P2X_QMAX) continue;
                     const double cost = sw_p2x_cost(bits(X, k, t), bits(X, k, u), X->nw[k], F / X->wc[k],
                                                     t, u, X->pc + X->off[k]);
                     if (cost < best) { best = cost; bk = k; }
@@ -78,7 +78,8 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
  * pred(cyc[i])) when its cost is negative, else 0. */
 #ifdef P2X_DEBUG
 #include <stdio.h>
-static long dbg_it, dbg_bf, dbg_walk;
+static long dbg_it, dbg_bf, dbg_walk, dbg_evals_cached, dbg_evals_full;
+static uint64_t dbg_dirty[SW_P2X_KMAX];
 #endif
 static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
 #ifdef P2X_DEBUG
@@ -244,6 +245,9 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
             v[q] = X->pc[q] * (double)S;
         }
     const double delta = SW_P2X_EPS * twin_detsum(v, A) / (double)T;
+#ifdef P2X_DEBUG
+    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
+#endif
     int32_t cyc[SW_TMAX + 1];
     int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)SW_P2X_MAX_MOVES);
     int32_t ncancel = 0;
@@ -253,6 +257,19 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
             const int32_t F = X->wc[ki];
             while (ncancel < SW_P2X_MAX_CANCEL) {
                 build_w(X, F, delta);
+#ifdef P2X_DEBUG
+                {   /* what a per-F cached W would recompute: rows/cols dirty since its last build */
+                    int32_t ncls = 0;
+                    for (int32_t k = 0; k < X->K; ++k) ncls += (X->wc[k] <= F && F % X->wc[k] == 0);
+                    const uint64_t dm = dbg_dirty[ki];
+                    long ent = 0;
+                    for (int32_t t = 0; t < T; ++t) for (int32_t u = 0; u < T; ++u)
+                        if (t != u && (((dm >> t) | (dm >> u)) & 1ull)) ++ent;
+                    dbg_evals_cached += ent * ncls;
+                    dbg_evals_full += (long)T * (T - 1) * ncls;
+                    dbg_dirty[ki] = 0;
+                }
+#endif
                 const int32_t len = find_cycle(X, F, cyc);
                 if (len == 0) break;
                 int32_t moves = 0; /* the cycle's job moves */
@@ -262,14 +279,22 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                 }
                 if (moves > SW_P2X_MAX_MOVES) break;
                 cancel(X, F, cyc, len, tmp);
+#ifdef P2X_DEBUG
+                for (int32_t i = 0; i < len; ++i) {
+                    const int32_t u = cyc[i], t = cyc[(i + 1) % len];
+                    if (u < T && t < T) for (int32_t q2 = 0; q2 < SW_P2X_KMAX; ++q2) dbg_dirty[q2] |= (1ull << t) | (1ull << u);
+                }
+#endif
                 ++ncancel;
                 changed = 1;
             }
         }
     }
 #ifdef P2X_DEBUG
-    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld\n", A, X->K, ncancel, dbg_bf, dbg_it);
-    dbg_bf = dbg_it = 0;
+    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld evals_full=%ld evals_cached=%ld\n", A, X->K,
+            ncancel, dbg_bf, dbg_it, dbg_evals_full, dbg_evals_cached);
+    dbg_bf = dbg_it = dbg_evals_full = dbg_evals_cached = 0;
+    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
 #endif
     /* back to the input order */
     for (int32_t q = 0; q < A; ++q) {

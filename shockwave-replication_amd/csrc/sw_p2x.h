@@ -13,7 +13,7 @@
  * round u changes the objective by c_j·(u − t).  For a load size F (each
  * class width present), the ROUND GRAPH has an edge t → u whose cost is the
  * cheapest way to move exactly F GPUs of load from t to u with jobs of ONE
- * class k (w_k | F): the q = F/w_k class-k jobs in t but not in u with the
+ * class k (w_k | F, q = F/w_k ≤ SW_P2X_QMAX): the q class-k jobs in t but not in u with the
  * largest c (u < t: they gain) or the smallest c (u > t: they lose).  A
  * virtual node V stands for free capacity: t → V is allowed when round t has
  * F free GPUs (t absorbs the load), V → u always (u's load leaves).  Every
@@ -46,6 +46,10 @@
 #define SW_P2X_EPS 2e-4        /* δ = ε·P2₀/T per edge                          */
 #endif
 #define SW_P2X_MAX_CANCEL 256  /* cancels per solve                              */
+#define SW_P2X_QMAX 4          /* jobs one edge moves (F / w_k ≤ this): a w8 job
+                                  against four w2 or two w4 jobs, not eight w1 —
+                                  the simulator-captured and headline fixtures
+                                  reach the same objectives without those      */
 #define SW_P2X_KMAX 8          /* width classes handled (more: the step is skipped) */
 #define SW_P2X_NONE 1.0e300    /* "no edge" cost                                 */
 #define SW_P2X_AMAX 4096       /* active jobs handled (more: the step is skipped) */

@@ -234,44 +234,47 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
 #undef BF_STAMP
 }
 
-/* sw_p2x_cost (sw_p2x.h) for classes of at most 256 jobs and q ≤ 8: the
- * and-not words are loaded once into registers, the selected ranks found
- * with register-only bit scans, then their c values read together and summed
- * in selection order (the same sum).  Other cases take sw_p2x_cost. */
-static __device__ __forceinline__ uint64_t p2x_sel4(const uint64_t (&xw)[4], int i) {
-    return i == 0 ? xw[0] : i == 1 ? xw[1] : i == 2 ? xw[2] : xw[3];
-}
+/* sw_p2x_cost (sw_p2x.h) for classes of at most 256 jobs (≤ 4 words) and
+ * q ≤ 4, branch-free: the and-not words are loaded once, listed in scan order
+ * (ascending words for u < t, descending otherwise), and each of the q picks
+ * takes the first set bit (lowest, or highest when descending) of the first
+ * non-empty word with selects only; the c loads are then issued together and
+ * summed in selection order (the same sum).  Other cases: sw_p2x_cost. */
 static __device__ __forceinline__ double p2x_cost_dev(const uint64_t* Bt, const uint64_t* Bu, int nw, int q,
                                                       int t, int u, const double* c) {
-    if (q > 8 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, q, t, u, c);
-    uint64_t xw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xw[i] = i < nw ? (Bt[i] & ~Bu[i]) : 0ull;
+    if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, q, t, u, c);
     const bool lo = u < t;
-    int wi = lo ? 0 : nw - 1;
-    uint64_t x = p2x_sel4(xw, wi);
-    int rk[8];
-    int got = 0;
+    uint64_t x[4];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        while (x == 0ull && (lo ? wi < nw - 1 : wi > 0)) {
-            wi += lo ? 1 : -1;
-            x = p2x_sel4(xw, wi);
-        }
-        const bool has = x != 0ull && g < q;
-        const int b = lo ? __builtin_ctzll(x) : 63 - __builtin_clzll(x);
-        rk[g] = 64 * wi + b;
-        x = has ? (lo ? x & (x - 1) : x & ~(1ull << b)) : x;
-        got += has;
+    for (int i = 0; i < 4; ++i) x[i] = i < nw ? (Bt[i] & ~Bu[i]) : 0ull;
+    /* y[s] = the s-th word in scan order */
+    uint64_t y[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int i = lo ? s : nw - 1 - s;
+        y[s] = (i >= 0 && i < 4) ? (i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]) : 0ull;
     }
-    if (got < q) return SW_P2X_NONE;
-    double cv[8];
+    const int avail = __popcll(y[0]) + __popcll(y[1]) + __popcll(y[2]) + __popcll(y[3]);
+    if (avail < q) return SW_P2X_NONE;
+    int rk[4];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) cv[g] = g < q ? c[rk[g]] : 0.0;
-    double sum = 0.0;
+    for (int g = 0; g < 4; ++g) {
+        const int s = y[0] ? 0 : y[1] ? 1 : y[2] ? 2 : 3;
+        const uint64_t ys = s == 0 ? y[0] : s == 1 ? y[1] : s == 2 ? y[2] : y[3];
+        const int b = lo ? __builtin_ctzll(ys) : 63 - __builtin_clzll(ys);
+        rk[g] = 64 * (lo ? s : nw - 1 - s) + (b & 63);
+        const uint64_t cl = ys & ~(1ull << (b & 63));
+        y[0] = s == 0 ? cl : y[0];
+        y[1] = s == 1 ? cl : y[1];
+        y[2] = s == 2 ? cl : y[2];
+        y[3] = s == 3 ? cl : y[3];
+    }
+    double cv[4];
 #pragma unroll
-    for (int g = 0; g < 8; ++g)
-        if (g < q) sum = sum + cv[g];
+    for (int g = 0; g < 4; ++g) cv[g] = c[g < q ? rk[g] : rk[0]];
+    double sum = cv[0];
+#pragma unroll
+    for (int g = 1; g < 4; ++g) sum = g < q ? sum + cv[g] : sum;
     return sum * (double)(u - t);
 }
 
@@ -471,7 +474,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             const int F = L->wc[ki];
             if (tid < SW_P2X_KMAX) {
                 const int wk = tid < K ? L->wc[tid] : 0;
-                L->fq[tid] = (wk > 0 && wk <= F && F % wk == 0) ? F / wk : 0;
+                L->fq[tid] = (wk > 0 && wk <= F && F % wk == 0 && F / wk <= SW_P2X_QMAX) ? F / wk : 0;
             }
             __syncthreads();
             bool all = true;

@@ -28,9 +28,9 @@
  * The batch kernel: instance blockIdx.x.  The per-job arrays live in the
  * workspace ws (SW_P2X_ARR_BYTES per job, L2-resident while the instance
  * runs) so that the LDS holds only the step's own state (~30 KB at 900 jobs ×
- * 30 rounds); at 94 VGPRs (5 waves per SIMD) two workgroups share a CU.
+ * 30 rounds); at ≤ 80 VGPRs (6 waves per SIMD) three workgroups share a CU.
  */
-__global__ __launch_bounds__(SW_BLOCK, 5) void sw_p2x_kernel(sw_batch_dev B, unsigned char* ws, int maxA,
+__global__ __launch_bounds__(SW_BLOCK, 6) void sw_p2x_kernel(sw_batch_dev B, unsigned char* ws, int maxA,
                                                              int maxT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int inst = blockIdx.x;
