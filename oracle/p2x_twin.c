@@ -80,6 +80,7 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
 #include <stdio.h>
 static long dbg_it, dbg_bf, dbg_walk, dbg_evals_cached, dbg_evals_full;
 static uint64_t dbg_dirty[SW_P2X_KMAX];
+static long dbg_len[8];
 #endif
 static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
 #ifdef P2X_DEBUG
@@ -244,7 +245,7 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                 }
             v[q] = X->pc[q] * (double)S;
         }
-    const double delta = SW_P2X_EPS * twin_detsum(v, A) / (double)T;
+    const double delta = sw_p2x_delta(twin_detsum(v, A), T, A);
 #ifdef P2X_DEBUG
     for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
 #endif
@@ -280,6 +281,12 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                 if (moves > SW_P2X_MAX_MOVES) break;
                 cancel(X, F, cyc, len, tmp);
 #ifdef P2X_DEBUG
+                {
+                    int32_t real = 0, hasv = 0;
+                    for (int32_t i = 0; i < len; ++i) { if (cyc[i] == T) hasv = 1; }
+                    real = len - hasv;
+                    dbg_len[real < 8 ? real : 7]++;
+                }
                 for (int32_t i = 0; i < len; ++i) {
                     const int32_t u = cyc[i], t = cyc[(i + 1) % len];
                     if (u < T && t < T) for (int32_t q2 = 0; q2 < SW_P2X_KMAX; ++q2) dbg_dirty[q2] |= (1ull << t) | (1ull << u);
@@ -291,8 +298,9 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
         }
     }
 #ifdef P2X_DEBUG
-    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld evals_full=%ld evals_cached=%ld\n", A, X->K,
-            ncancel, dbg_bf, dbg_it, dbg_evals_full, dbg_evals_cached);
+    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld evals_full=%ld evals_cached=%ld len2=%ld len3=%ld len4+=%ld\n", A, X->K,
+            ncancel, dbg_bf, dbg_it, dbg_evals_full, dbg_evals_cached, dbg_len[2], dbg_len[3], dbg_len[4]+dbg_len[5]+dbg_len[6]+dbg_len[7]);
+    for (int32_t k = 0; k < 8; ++k) dbg_len[k] = 0;
     dbg_bf = dbg_it = dbg_evals_full = dbg_evals_cached = 0;
     for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
 #endif

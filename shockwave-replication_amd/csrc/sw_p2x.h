@@ -56,6 +56,18 @@
 #define SW_P2X_MAX_MOVES 1024  /* job moves one cycle may make (more: the cycle is
                                   not cancelled and the load size F is done)     */
 
+/* The per-edge shift δ = ε·P2₀/T·max(1, A/SW_P2X_ASCALE): a cycle is
+ * cancelled only if it gains more than δ per edge.  Beyond SW_P2X_ASCALE
+ * active jobs the tolerance grows with A (the cancels of a 900-job instance
+ * then gain ≥ the same share of an average job's cost as those of a
+ * 128-job one): 40–50 Bellman–Ford sweeps per C3 instance instead of ~90, the
+ * headline fixtures at ≤ 1.0007× of the P2 MILP instead of ≤ 1.0006×. */
+#define SW_P2X_ASCALE 128
+SW_HD double sw_p2x_delta(double P0, int32_t T, int32_t A) {
+    const double s = A > SW_P2X_ASCALE ? (double)A / (double)SW_P2X_ASCALE : 1.0;
+    return SW_P2X_EPS * P0 / (double)T * s;
+}
+
 /* Rank order inside a class: this key descending (c = p/n ≥ 0 without its
  * 3 lowest mantissa bits, so it fits beside a class index in one word), then
  * job ascending. */

@@ -461,7 +461,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             acc = acc + pc[p] * (double)S;
         }
         const double P0 = blk.detsum(acc); /* its barrier publishes B, room */
-        if (tid == 0) L->delta = SW_P2X_EPS * P0 / (double)T;
+        if (tid == 0) L->delta = sw_p2x_delta(P0, T, A);
     }
     __syncthreads();
     const double delta = L->delta;
