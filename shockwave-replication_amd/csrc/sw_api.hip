@@ -27,6 +27,7 @@
 extern "C" size_t sw_plan_kernel_lds_bytes(int one);
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream);
+extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream);
 extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, unsigned char* ws,
                                     hipStream_t stream);
 
@@ -141,7 +142,7 @@ void sw_destroy(sw_handle* h) {
     h->d_planned.release(); h->d_d.release(); h->d_R.release(); h->d_p.release();
     h->d_plan.release(); h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
     h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_out.release(); h->d_stamps.release();
-    h->d_masks.release(); h->d_p2ws.release();
+    h->d_masks.release(); h->d_p2ws.release(); h->d_nb.release(); h->d_lvl.release();
     h->h_w.release(); h->h_F.release(); h->h_E.release(); h->h_planned.release();
     h->h_d.release(); h->h_R.release(); h->h_p.release(); h->h_plan.release(); h->h_out.release();
     for (hipEvent_t ev : h->ev_pool)
@@ -184,7 +185,8 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
     if (h->d_inst.reserve(std::max(count, 1)) || h->d_out.reserve(std::max(count, 1)) ||
         h->d_w.reserve(Jz) || h->d_F.reserve(Jz) || h->d_E.reserve(Jz) ||
         h->d_planned.reserve(Jz) || h->d_d.reserve(Jz) || h->d_R.reserve(Jz) ||
-        h->d_p.reserve(Jz) || h->d_masks.reserve(Jz) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
+        h->d_p.reserve(Jz) || h->d_masks.reserve(Jz) || h->d_nb.reserve(Jz) ||
+        h->d_lvl.reserve(std::max(count, 1)) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS || maxT > 32) {
         const int KT = maxT <= 32 ? 32 : 64;
@@ -292,6 +294,8 @@ int sw_batch_run(sw_handle* h) {
     B.planned = h->d_planned.p;
     B.masks = h->d_masks.p;
     B.out = h->d_out.p;
+    B.nb = h->d_nb.p;
+    B.lvl = h->d_lvl.p;
 #ifdef SW_STAMPS
     B.stamps = h->d_stamps.p;
 #endif
@@ -308,8 +312,16 @@ int sw_batch_run(sw_handle* h) {
         if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], h->stream));
     }
-    hipError_t e = sw_launch_plan(&B, B.KT, one, lds, h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "sw_plan_kernel launch");
+    /* on-chip batches: level-search kernel, pack kernel, full kernel for the
+     * instances the pack kernel leaves (sw_kernels.hip); otherwise the full
+     * kernel for every instance */
+#ifdef SW_STAMPS
+    const bool split = false; /* diagnostic builds time the phases inside the full kernel */
+#else
+    const bool split = one;
+#endif
+    hipError_t e = split ? sw_launch_split(&B, h->stream) : sw_launch_plan(&B, B.KT, one, lds, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");
     if (h->timing) {
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], h->stream));
         SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], h->stream));

@@ -51,6 +51,15 @@ struct sw_ws_dev {
  * PPL = ⌈A/64⌉) reach up to A + 62, so each slot array holds N + 64 entries */
 #define SW_WS_PAD_U64 192
 
+/* Per-instance result of the level-search kernel (sw_level_kernel), read by
+ * the pack kernel (sw_pack_kernel). */
+struct sw_lvl_dev {
+    double U, M, bound; /* utility and makespan of the best level's counts, P1 bound */
+    int64_t passes;
+};
+/* out.status of an instance the pack kernel left to the full plan kernel */
+#define SW_STATUS_SLOW_MARK 0x40000000
+
 struct sw_batch_dev {
     const sw_inst_dev* inst;
     int32_t count;
@@ -65,6 +74,9 @@ struct sw_batch_dev {
     int32_t* planned;
     uint64_t* masks;
     sw_out_dev* out;
+    uint8_t* nb;      /* level-search counts per job (sw_level_kernel → sw_pack_kernel) */
+    sw_lvl_dev* lvl;  /* per instance                                              */
+    int32_t only_slow; /* sw_plan_kernel: solve only instances marked SW_STATUS_SLOW_MARK */
     sw_ws_dev ws;
     uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][16] cycles (8…13: pack round-loop phases) */
 };

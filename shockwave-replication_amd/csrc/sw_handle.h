@@ -80,6 +80,8 @@ struct sw_handle {
     DevBuf<sw_jobc> d_ws_jc;
     DevBuf<sw_out_dev> d_out;
     DevBuf<uint64_t> d_masks;     /* final round masks (plan kernel → P2 exchange) */
+    DevBuf<uint8_t> d_nb;         /* level-search counts (level kernel → pack kernel) */
+    DevBuf<sw_lvl_dev> d_lvl;     /* level-search results per instance                */
     DevBuf<unsigned char> d_p2ws; /* P2 exchange arrays of instances > SW_LDS_JOBS jobs */
     DevBuf<uint64_t> d_stamps; /* SW_STAMPS diagnostic builds */
     /* pinned staging */

@@ -125,6 +125,7 @@ struct Ctx {
     double k, A;
     double inv_delta; /* 1 / Δ: the slope of g(n) ≈ R − Δ·n (d·rate = Δ) */
     int64_t passes;
+    double lsU, lsM; /* utility / makespan of the level search's best counts */
     const sw_inst_dev* inst;
     const double* beta; /* LDS */
     const double* ell;  /* LDS */
@@ -789,6 +790,8 @@ struct Ctx {
                 phase = 5;
             }
         }
+        lsU = best.U;
+        lsM = best.Mact;
         __syncthreads();
         return ret;
     }
@@ -990,7 +993,7 @@ struct Ctx {
             uint64_t k1;
             uint32_t k2;
             if (MODE == 4) {
-                k1 = sw_ratio_key(p_in[j] / (double)(nj * jc(j, s).w));
+                k1 = sw_ratio_key(p_in[j] / (double)(nj * w_in[j]));
                 k2 = 0;
             } else if (MODE != 2 && MODE != 5) {
                 const double lvl = gval(j, s, nj - 1);
@@ -1392,9 +1395,282 @@ __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
     return s;
 }
 
+/* LDS of the level-search kernel: the setup's key staging window (whose
+ * space the per-job level-search bytes reuse afterwards) and the per-job
+ * constants. */
+__host__ __device__ constexpr size_t sw_level_lds_bytes() {
+    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    return r16(sizeof(sw_xchg)) + r16(sizeof(double) * 3 * SW_BMAX) +
+           r16(sizeof(float) * SW_JPT * 4 * SW_BLOCK) + SW_JOB_LDS_BYTES;
+}
+
+/* LDS of the pack kernel: pack and repair state, counts, masks, sort exchange. */
+__host__ __device__ constexpr size_t sw_pack_lds_bytes() {
+    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t NJ = SW_LDS_JOBS;
+    return r16(sizeof(sw_xchg)) + r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) +
+           r16(sizeof(sw_repair_t)) + 3 * r16(NJ) + 2 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
+}
+
+/*
+ * The level-search kernel (on-chip instances): setup and the P1 level search
+ * of solve_instance's first iteration, nothing else; the counts and the best
+ * level's utility, makespan, bound and passes go to HBM for sw_pack_kernel.
+ * Without the packer's state its LDS is ~85 KB.
+ */
+template <int KT>
+__device__ __forceinline__ void level_instance(const sw_batch_dev& B, unsigned char* smem, int inst_) {
+    const sw_inst_dev* I = &B.inst[inst_];
+    Ctx<KT, true> c;
+    c.inst = I;
+    c.N = I->N;
+    c.T = I->T;
+    c.G = I->G;
+    c.nb = I->nb;
+    c.C = (int64_t)I->G * I->T;
+    c.k = I->k;
+    c.inv_delta = 1.0 / I->delta;
+    c.passes = 0;
+    c.q = (c.N + SW_BLOCK - 1) / SW_BLOCK;
+    const int N = c.N;
+    const int64_t jo = I->job_off;
+    c.w_in = B.w + jo;
+    c.p_in = B.p + jo;
+#ifdef SW_STAMPS
+    c.swp = nullptr;
+    c.lsp = nullptr;
+#endif
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        unsigned char* p = smem + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    c.blk.X = (sw_xchg*)carve(sizeof(sw_xchg));
+    c.blk.par = 0;
+    double* bt = (double*)carve(sizeof(double) * 3 * SW_BMAX);
+    c.beta = bt;
+    c.ell = bt + SW_BMAX;
+    c.slope = bt + 2 * SW_BMAX;
+    if (threadIdx.x < SW_BMAX) {
+        const int b = (int)threadIdx.x;
+        bt[b] = I->beta[b];
+        bt[SW_BMAX + b] = I->ell[b];
+        bt[2 * SW_BMAX + b] = b < I->nb - 1 ? (I->ell[b + 1] - I->ell[b]) / (I->beta[b + 1] - I->beta[b])
+                                            : 0.0;
+    }
+    /* the setup's staging window; the level search's per-job bytes use the
+     * same space once the key rows are in registers */
+    unsigned char* stage = carve(sizeof(float) * SW_JPT * 4 * SW_BLOCK);
+    c.sbuf = reinterpret_cast<uint64_t*>(stage);
+    const int NJ = SW_LDS_JOBS;
+    c.ncur = stage;
+    c.lcur = stage + NJ;
+    c.tkcur = stage + 2 * NJ;
+    c.nbest = stage + 3 * NJ;
+    c.tiecur = stage + 4 * NJ;
+    c.placed = c.placed2 = c.nfin = nullptr;
+    c.ycur = c.ybest = c.y2 = nullptr;
+    c.pst = nullptr;
+    c.pord = nullptr;
+    c.pmask = nullptr;
+    c.PL = nullptr;
+    c.H = c.SH = c.caps = nullptr;
+    c.pwc = 0;
+    c.misc = nullptr;
+    c.rep = nullptr;
+    c.gkeys = nullptr;
+    c.gjc = nullptr;
+    c.JL.carve(carve);
+    for (int j = threadIdx.x; j < NJ; j += SW_BLOCK)
+        c.JL.put(j, j < N ? sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
+                                         B.E[jo + j], B.R[jo + j], B.p[jo + j])
+                          : sw_make_jobc(1, 1, 1.0, 1, 1.0, 0, 1, 0.0, 0.0));
+    if (off != sw_level_lds_bytes()) __builtin_trap();
+    __syncthreads();
+    c.setup(); /* its closing barrier: the staging window is free */
+    const double bound = c.level_search();
+    c.for_jobs([&](int j, int s) {
+        (void)s;
+        B.nb[jo + j] = c.nbest[j];
+    });
+    if (threadIdx.x == 0) {
+        sw_lvl_dev v;
+        v.U = c.lsU;
+        v.M = c.lsM;
+        v.bound = bound;
+        v.passes = c.passes;
+        B.lvl[inst_] = v;
+    }
+}
+
+/* The 16-byte plan stores of the emit (shockwave.py:390-398 reads x[j][t]):
+ * the instance's N·T-byte range written with aligned 16-byte stores, each
+ * thread expanding 16 consecutive bytes from the round masks ym. */
+__device__ __forceinline__ void emit_plan_bytes(uint8_t* plan, const uint64_t* ym, int N, int T) {
+    const int32_t nbytes = N * T;
+    const int32_t mis = (int32_t)(reinterpret_cast<uintptr_t>(plan) & 15u);
+    const int32_t head = min(nbytes, (16 - mis) & 15);
+    const int32_t nch = (nbytes - head) >> 4;
+    auto byte_at = [&](int32_t b) {
+        const int32_t j = b / T;
+        return (uint8_t)((ym[j] >> (b - j * T)) & 1ull);
+    };
+    for (int32_t b = threadIdx.x; b < head; b += SW_BLOCK) plan[b] = byte_at(b);
+    for (int32_t b = head + nch * 16 + threadIdx.x; b < nbytes; b += SW_BLOCK) plan[b] = byte_at(b);
+    uint4* dst = reinterpret_cast<uint4*>(plan + head);
+    for (int32_t ci = threadIdx.x; ci < nch; ci += SW_BLOCK) {
+        const int32_t b0 = head + ci * 16;
+        int32_t j = b0 / T, t = b0 - j * T;
+        uint64_t m = ym[j];
+        uint32_t wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            wv[k >> 2] |= (uint32_t)((m >> t) & 1ull) << ((k & 3) * 8);
+            if (++t == T) {
+                t = 0;
+                ++j;
+                if (k < 15 && j < N) m = ym[j];
+            }
+        }
+        dst[ci] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+}
+
+/*
+ * The pack kernel (on-chip instances): solve_instance's path after the level
+ * search when the density order places the counts (with its width-profile
+ * repair if it strands rounds) — then that placement is P1's and P2's, and
+ * the emit's utility and makespan are the level search's (same counts, same
+ * sums).  Otherwise the instance is marked SW_STATUS_SLOW_MARK and
+ * sw_plan_kernel solves it whole.  No per-job constants, no key rows: ~54 KB
+ * of LDS and few registers, so two instances share a CU.
+ */
+__device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned char* smem, int inst_) {
+    const sw_inst_dev* I = &B.inst[inst_];
+    Ctx<32, true> c;
+    c.inst = I;
+    c.N = I->N;
+    c.T = I->T;
+    c.G = I->G;
+    c.nb = I->nb;
+    c.C = (int64_t)I->G * I->T;
+    c.k = I->k;
+    c.inv_delta = 1.0 / I->delta;
+    const sw_lvl_dev lv = B.lvl[inst_];
+    c.passes = lv.passes;
+    c.q = (c.N + SW_BLOCK - 1) / SW_BLOCK;
+    const int N = c.N, T = c.T;
+    const int64_t jo = I->job_off;
+    c.w_in = B.w + jo;
+    c.p_in = B.p + jo;
+#ifdef SW_STAMPS
+    c.swp = nullptr;
+    c.lsp = nullptr;
+#endif
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        unsigned char* p = smem + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    c.blk.X = (sw_xchg*)carve(sizeof(sw_xchg));
+    c.blk.par = 0;
+    c.beta = c.ell = c.slope = nullptr;
+    c.PL = (sw_pack_lds*)carve(sizeof(sw_pack_lds));
+    c.H = c.PL->H[0];
+    c.SH = c.PL->SH[0];
+    c.caps = c.PL->H[1];
+    c.pwc = 0;
+    c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
+    c.rep = (sw_repair_t*)carve(sizeof(sw_repair_t));
+    const int NJ = SW_LDS_JOBS;
+    c.nbest = carve(NJ);
+    c.placed = carve(NJ);
+    c.placed2 = carve(NJ);
+    c.ncur = c.lcur = c.tkcur = c.nfin = c.tiecur = nullptr;
+    c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
+    c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
+    c.ybest = nullptr;
+    c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 4 * SW_JPT * SW_BLOCK);
+    c.pst = nullptr;
+    c.pord = nullptr;
+    c.pmask = nullptr;
+    c.gkeys = nullptr;
+    c.gjc = nullptr;
+    if (off != sw_pack_lds_bytes()) __builtin_trap();
+    c.for_jobs([&](int j, int s) {
+        (void)s;
+        c.nbest[j] = B.nb[jo + j];
+    });
+    /* twin_plan_solve's first pack: the density order (mode 4) */
+    c.pack(4, c.nbest, c.ycur, c.placed);
+    int64_t def_l = 0;
+    c.for_jobs([&](int j, int s) {
+        (void)s;
+        def_l += (int64_t)c.w_in[j] * (c.nbest[j] - c.placed[j]);
+    });
+    int64_t dfc = c.blk.sum(def_l);
+    c.passes++;
+    int32_t status = 0;
+    if (dfc != 0 && c.repair_pack(c.nbest, c.ycur, c.placed, c.y2, c.placed2)) {
+        c.for_jobs([&](int j, int s) {
+            (void)s;
+            c.ycur[j] = c.y2[j];
+        });
+        c.passes++;
+        dfc = 0;
+        status |= SW_STATUS_P2_REPAIRED;
+    }
+    sw_out_dev* out = &B.out[inst_];
+    if (dfc != 0) { /* the other P1 orders, re-solves, fill: sw_plan_kernel */
+        if (threadIdx.x == 0) out->status = SW_STATUS_SLOW_MARK;
+        return;
+    }
+    /* emit (solve_instance's, with the level search's U and M) */
+    int64_t any_l = 0;
+    double p2 = 0.0;
+    c.for_jobs([&](int j, int s) {
+        (void)s;
+        const uint64_t m = c.ycur[j];
+        const int cnt = __popcll(m);
+        any_l += (cnt > 0);
+        double term = 0.0;
+        if (cnt > 0) {
+            const int64_t Ssum = (int64_t)__popcll(m & 0xAAAAAAAAAAAAAAAAull) +
+                                 2 * (int64_t)__popcll(m & 0xCCCCCCCCCCCCCCCCull) +
+                                 4 * (int64_t)__popcll(m & 0xF0F0F0F0F0F0F0F0ull) +
+                                 8 * (int64_t)__popcll(m & 0xFF00FF00FF00FF00ull) +
+                                 16 * (int64_t)__popcll(m & 0xFFFF0000FFFF0000ull) +
+                                 32 * (int64_t)__popcll(m & 0xFFFFFFFF00000000ull);
+            term = ((double)Ssum / (double)cnt) * c.p_in[j];
+        }
+        p2 = p2 + term;
+        B.planned[jo + j] = cnt;
+        B.masks[jo + j] = m;
+    });
+    const double P2 = c.blk.detsum(p2);
+    const int64_t any_n = c.blk.sum(any_l); /* its barrier: every mask row is final */
+    if (any_n == 0) status |= SW_STATUS_NO_PLANNED;
+    emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
+    if (threadIdx.x == 0) {
+        sw_out_dev o;
+        o.objective = lv.U - c.k * lv.M;
+        o.utility = lv.U;
+        o.makespan = lv.M;
+        o.p2_objective = P2;
+        o.bound = lv.bound;
+        o.iters = (int32_t)c.passes;
+        o.status = status;
+        *out = o;
+    }
+}
+
 template <int KT, bool ONE>
 __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned char* smem,
                                                          int inst_) {
+    /* the slow-path launch after sw_pack_kernel: only the marked instances */
+    if (B.only_slow && !(B.out[inst_].status & SW_STATUS_SLOW_MARK)) return;
     const sw_inst_dev* I = &B.inst[inst_];
 #ifdef SW_STAMPS
     /* placement diagnostics: 100 MHz wall clock at entry / exit, HW_ID, XCC_ID */
@@ -1741,42 +2017,13 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.blk.detsum2_max_cnt(fs, p2, gm, (int32_t)any_l, U, P2, Mact, any_n);
     const bool any = any_n > 0;
     if (!any) status |= SW_STATUS_NO_PLANNED;
-    /* The plan bytes (shockwave.py:390-398 reads x[j][t]): the instance's
-     * N·T-byte range written with aligned 16-byte stores, each thread
-     * expanding 16 consecutive bytes from the round masks (a chunk spans at
-     * most ⌈16/T⌉ + 1 jobs), byte stores only for the unaligned head
-     * and tail — instead of every thread storing its own jobs' bytes one at
-     * a time (strided byte stores that inflated WRITE_SIZE by ~1.6x). */
-    {
-        const uint64_t* ym = ok2 ? c.y2 : c.ybest;
-        const int32_t nbytes = N * T;
-        const int32_t mis = (int32_t)(reinterpret_cast<uintptr_t>(plan) & 15u);
-        const int32_t head = min(nbytes, (16 - mis) & 15);
-        const int32_t nch = (nbytes - head) >> 4;
-        auto byte_at = [&](int32_t b) {
-            const int32_t j = b / T;
-            return (uint8_t)((ym[j] >> (b - j * T)) & 1ull);
-        };
-        for (int32_t b = threadIdx.x; b < head; b += SW_BLOCK) plan[b] = byte_at(b);
-        for (int32_t b = head + nch * 16 + threadIdx.x; b < nbytes; b += SW_BLOCK) plan[b] = byte_at(b);
-        uint4* dst = reinterpret_cast<uint4*>(plan + head);
-        for (int32_t ci = threadIdx.x; ci < nch; ci += SW_BLOCK) {
-            const int32_t b0 = head + ci * 16;
-            int32_t j = b0 / T, t = b0 - j * T;
-            uint64_t m = ym[j];
-            uint32_t wv[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                wv[k >> 2] |= (uint32_t)((m >> t) & 1ull) << ((k & 3) * 8);
-                if (++t == T) {
-                    t = 0;
-                    ++j;
-                    if (k < 15 && j < N) m = ym[j];
-                }
-            }
-            dst[ci] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        }
-    }
+    /* The plan bytes (shockwave.py:390-398 reads x[j][t]) with aligned
+     * 16-byte stores, each thread expanding 16 consecutive bytes from the
+     * round masks (a chunk spans at most ⌈16/T⌉ + 1 jobs), byte stores only
+     * for the unaligned head and tail — instead of every thread storing its
+     * own jobs' bytes one at a time (strided byte stores that inflated
+     * WRITE_SIZE by ~1.6x). */
+    emit_plan_bytes(plan, ok2 ? c.y2 : c.ybest, N, T);
     SW_STAMP(5);
     if (threadIdx.x == 0) {
         sw_out_dev o;
@@ -1813,8 +2060,34 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
     solve_instance<KT, ONE>(B, sw_smem, blockIdx.x);
 }
 
+template <int KT>
+__global__ __launch_bounds__(SW_BLOCK) void sw_level_kernel(sw_batch_dev B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
+    level_instance<KT>(B, sw_smem, blockIdx.x);
+}
+
+/* ≤ 128 VGPRs: two 512-thread workgroups per CU (LDS ~54 KB each) */
+__global__ __launch_bounds__(SW_BLOCK, 4) void sw_pack_kernel(sw_batch_dev B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
+    pack_instance(B, sw_smem, blockIdx.x);
+}
+
 /* LDS bytes the kernel needs (solve_instance checks its carve-up against it). */
 extern "C" size_t sw_plan_kernel_lds_bytes(int one) { return sw_plan_lds_bytes(one != 0); }
+
+/* The split path for on-chip batches (every instance N ≤ SW_LDS_JOBS and
+ * T ≤ 32): level search, then pack + emit, then the full kernel for the
+ * instances the pack kernel marked (B->only_slow set by the caller). */
+extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream) {
+    dim3 grid(B->count), block(SW_BLOCK);
+    B->only_slow = 0;
+    hipLaunchKernelGGL((sw_level_kernel<32>), grid, block, sw_level_lds_bytes(), stream, *B);
+    hipLaunchKernelGGL(sw_pack_kernel, grid, block, sw_pack_lds_bytes(), stream, *B);
+    B->only_slow = 1;
+    hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, sw_plan_lds_bytes(true), stream, *B);
+    B->only_slow = 0;
+    return hipGetLastError();
+}
 
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream) {
