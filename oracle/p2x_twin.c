@@ -81,6 +81,11 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
 static long dbg_it, dbg_bf, dbg_walk, dbg_evals_cached, dbg_evals_full;
 static uint64_t dbg_dirty[SW_P2X_KMAX];
 static long dbg_len[8];
+static double dbg_pot[SW_TMAX + 1];
+static int dbg_pot_ok;
+static double dbg_potF[SW_P2X_KMAX][SW_TMAX + 1];
+static int dbg_potF_ok[SW_P2X_KMAX];
+static long dbg_skippable, dbg_cert;
 #endif
 static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
 #ifdef P2X_DEBUG
@@ -118,7 +123,13 @@ static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
             np[T] = bp;
             changed |= best < d[T];
         }
-        if (!changed) return 0;
+        if (!changed) {
+#ifdef P2X_DEBUG
+            for (int32_t x = 0; x <= T; ++x) dbg_pot[x] = d[x];
+            dbg_pot_ok = 1;
+#endif
+            return 0;
+        }
         for (int32_t x = 0; x <= T; ++x) { d[x] = nd[x]; pr[x] = np[x]; }
         /* checked after the odd sweeps and the last one (after the first
          * sweep every predecessor is a later round: no cycle can exist) */
@@ -271,7 +282,32 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                     dbg_dirty[ki] = 0;
                 }
 #endif
+#ifdef P2X_DEBUG
+                int skippable = 0;
+                if (dbg_potF_ok[ki]) { /* would the stored potential certify "no negative cycle"? */
+                    const double* P = dbg_potF[ki];
+                    skippable = 1;
+                    for (int32_t t = 0; t < T && skippable; ++t) {
+                        for (int32_t u = 0; u < T; ++u) {
+                            const double w = X->W[t * T + u];
+                            if (t != u && w < SW_P2X_NONE && w + P[t] - P[u] < 0.0) { skippable = 0; break; }
+                        }
+                        if (X->room[t] >= F && P[t] - P[T] < 0.0) skippable = 0; /* t -> V */
+                        if (P[T] - P[t] < 0.0) skippable = 0;                    /* V -> t */
+                    }
+                }
+                dbg_pot_ok = 0;
+#endif
                 const int32_t len = find_cycle(X, F, cyc);
+#ifdef P2X_DEBUG
+                if (len == 0) {
+                    dbg_cert++;
+                    dbg_skippable += skippable;
+                    if (dbg_pot_ok) { for (int32_t x = 0; x <= T; ++x) dbg_potF[ki][x] = dbg_pot[x]; dbg_potF_ok[ki] = 1; }
+                } else {
+                    dbg_potF_ok[ki] = 0;
+                }
+#endif
                 if (len == 0) break;
                 int32_t moves = 0; /* the cycle's job moves */
                 for (int32_t i = 0; i < len; ++i) {
@@ -301,6 +337,9 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
     fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld evals_full=%ld evals_cached=%ld len2=%ld len3=%ld len4+=%ld\n", A, X->K,
             ncancel, dbg_bf, dbg_it, dbg_evals_full, dbg_evals_cached, dbg_len[2], dbg_len[3], dbg_len[4]+dbg_len[5]+dbg_len[6]+dbg_len[7]);
     for (int32_t k = 0; k < 8; ++k) dbg_len[k] = 0;
+    fprintf(stderr, "    certifications=%ld skippable=%ld\n", dbg_cert, dbg_skippable);
+    dbg_cert = dbg_skippable = 0;
+    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_potF_ok[k] = 0;
     dbg_bf = dbg_it = dbg_evals_full = dbg_evals_cached = 0;
     for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
 #endif

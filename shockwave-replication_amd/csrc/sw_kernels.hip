@@ -117,7 +117,9 @@ struct sw_job_lds {
 /* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = SW_JPT · SW_BLOCK) */
 #define SW_JPT 2
 
-template <int KT, bool ONE>
+/* SMALL: the pack kernel's context — every pack has at most SW_BLOCK active
+ * jobs (one position per thread), so the 1024-position paths compile out. */
+template <int KT, bool ONE, bool SMALL = false>
 struct Ctx {
     /* instance scalars (uniform) */
     int32_t N, T, G, nb, q;
@@ -1057,7 +1059,7 @@ struct Ctx {
                                  ? (khi[s] << 11) | (uint64_t)(2047u - (0xFFFFFFFFu - (uint32_t)klo[s]))
                                  : 0ull;
             }
-            if (A_ <= SW_BLOCK) {
+            if (SMALL || A_ <= SW_BLOCK) {
                 /* at most one position per thread (a C3 instance places ~1/3
                  * of its jobs): compact the active keys through LDS, sort
                  * SW_BLOCK of them one per thread (half the network of the
@@ -1104,6 +1106,7 @@ struct Ctx {
                 }
                 __syncthreads();
             } else {
+                if constexpr (!SMALL) {
                 if (ratio) sort_regs64(khi);
                 else sort_regs(khi, klo);
 #ifdef SW_STAMPS
@@ -1140,6 +1143,7 @@ struct Ctx {
                     }
                 }
                 __syncthreads();
+                            }
             }
         } else {
             int NPg = 1;
@@ -1409,7 +1413,7 @@ __host__ __device__ constexpr size_t sw_pack_lds_bytes() {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     const size_t NJ = SW_LDS_JOBS;
     return r16(sizeof(sw_xchg)) + r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) +
-           r16(sizeof(sw_repair_t)) + 3 * r16(NJ) + 2 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK);
+           r16(sizeof(sw_repair_t)) + 3 * r16(NJ) + 2 * r16(8 * NJ) + r16(8 * 6 * SW_BLOCK);
 }
 
 /*
@@ -1543,12 +1547,14 @@ __device__ __forceinline__ void emit_plan_bytes(uint8_t* plan, const uint64_t* y
  * repair if it strands rounds) — then that placement is P1's and P2's, and
  * the emit's utility and makespan are the level search's (same counts, same
  * sums).  Otherwise the instance is marked SW_STATUS_SLOW_MARK and
- * sw_plan_kernel solves it whole.  No per-job constants, no key rows: ~54 KB
- * of LDS and few registers, so two instances share a CU.
+ * sw_plan_kernel solves it whole, as it does an instance with more than
+ * SW_BLOCK jobs to place (one position per thread here).  No per-job
+ * constants, no key rows: ~47 KB of LDS and ≤ 80 VGPRs, so three instances
+ * share a CU.
  */
 __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned char* smem, int inst_) {
     const sw_inst_dev* I = &B.inst[inst_];
-    Ctx<32, true> c;
+    Ctx<32, true, true> c;
     c.inst = I;
     c.N = I->N;
     c.T = I->T;
@@ -1592,17 +1598,24 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.ybest = nullptr;
-    c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 4 * SW_JPT * SW_BLOCK);
+    c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 6 * SW_BLOCK); /* compaction + sort_one exchange */
     c.pst = nullptr;
     c.pord = nullptr;
     c.pmask = nullptr;
     c.gkeys = nullptr;
     c.gjc = nullptr;
     if (off != sw_pack_lds_bytes()) __builtin_trap();
+    int64_t act_l = 0;
     c.for_jobs([&](int j, int s) {
         (void)s;
         c.nbest[j] = B.nb[jo + j];
+        act_l += c.nbest[j] > 0;
     });
+    sw_out_dev* out = &B.out[inst_];
+    if (c.blk.sum(act_l) > SW_BLOCK) { /* more positions than threads: sw_plan_kernel */
+        if (threadIdx.x == 0) out->status = SW_STATUS_SLOW_MARK;
+        return;
+    }
     /* twin_plan_solve's first pack: the density order (mode 4) */
     c.pack(4, c.nbest, c.ycur, c.placed);
     int64_t def_l = 0;
@@ -1622,7 +1635,6 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
         dfc = 0;
         status |= SW_STATUS_P2_REPAIRED;
     }
-    sw_out_dev* out = &B.out[inst_];
     if (dfc != 0) { /* the other P1 orders, re-solves, fill: sw_plan_kernel */
         if (threadIdx.x == 0) out->status = SW_STATUS_SLOW_MARK;
         return;
@@ -2066,8 +2078,8 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_level_kernel(sw_batch_dev B) {
     level_instance<KT>(B, sw_smem, blockIdx.x);
 }
 
-/* ≤ 128 VGPRs: two 512-thread workgroups per CU (LDS ~54 KB each) */
-__global__ __launch_bounds__(SW_BLOCK, 4) void sw_pack_kernel(sw_batch_dev B) {
+/* ≤ 80 VGPRs: three 512-thread workgroups per CU (LDS ~47 KB each) */
+__global__ __launch_bounds__(SW_BLOCK, 6) void sw_pack_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
     pack_instance(B, sw_smem, blockIdx.x);
 }

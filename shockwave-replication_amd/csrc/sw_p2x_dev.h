@@ -468,10 +468,21 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     P2X_STAMP(2);
     /* ---- cancelling ---- */
     int ncancel = 0;
+    /* cert[k]: the cancel count when load size k last had no cycle — while
+     * nothing was cancelled since, its graph is unchanged and a repeat
+     * Bellman–Ford would find none again, so the repeat pass skips it (the
+     * specification's result, without the work) */
+    int cert[SW_P2X_KMAX];
+#pragma unroll
+    for (int k = 0; k < SW_P2X_KMAX; ++k) cert[k] = -1;
     for (bool changed = true; changed && ncancel < SW_P2X_MAX_CANCEL;) {
         changed = false;
         for (int ki = 0; ki < K && ncancel < SW_P2X_MAX_CANCEL; ++ki) {
             const int F = L->wc[ki];
+            int certk = -1;
+#pragma unroll
+            for (int k = 0; k < SW_P2X_KMAX; ++k) certk = k == ki ? cert[k] : certk;
+            if (certk == ncancel) continue; /* uniform */
             if (tid < SW_P2X_KMAX) {
                 const int wk = tid < K ? L->wc[tid] : 0;
                 L->fq[tid] = (wk > 0 && wk <= F && F % wk == 0 && F / wk <= SW_P2X_QMAX) ? F / wk : 0;
@@ -488,7 +499,11 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                 p2x_find_cycle(L, W, T, F, sp);
                 P2X_STAMP(4);
                 const int len = L->len;
-                if (len == 0) break;
+                if (len == 0) {
+#pragma unroll
+                    for (int k = 0; k < SW_P2X_KMAX; ++k) cert[k] = k == ki ? ncancel : cert[k];
+                    break;
+                }
                 /* the cycle's moves, all selected before any is applied: wave 0,
                  * one lane per edge (edge i: pred(cyc[i]) → cyc[i]) */
                 if (wave_id() == 0) {

@@ -30,7 +30,7 @@
  * runs) so that the LDS holds only the step's own state (~30 KB at 900 jobs ×
  * 30 rounds); at ≤ 80 VGPRs (6 waves per SIMD) three workgroups share a CU.
  */
-__global__ __launch_bounds__(SW_BLOCK, 6) void sw_p2x_kernel(sw_batch_dev B, unsigned char* ws, int maxA,
+__global__ __launch_bounds__(SW_BLOCK, 8) void sw_p2x_kernel(sw_batch_dev B, unsigned char* ws, int maxA,
                                                              int maxT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int inst = blockIdx.x;
