@@ -22,6 +22,9 @@
 #include "sw_handle.h"
 #include "sw_validate.h"
 
+/* batches above this many instances take the split kernels (MI355X: 256 CUs) */
+constexpr int kSplitMinCount = 256;
+
 #define SW_P2X_ARR_BYTES 24 /* sw_p2x_dev.h: exchange workspace bytes per job */
 
 extern "C" size_t sw_plan_kernel_lds_bytes(int one);
@@ -312,13 +315,16 @@ int sw_batch_run(sw_handle* h) {
         if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], h->stream));
     }
-    /* on-chip batches: level-search kernel, pack kernel, full kernel for the
-     * instances the pack kernel leaves (sw_kernels.hip); otherwise the full
-     * kernel for every instance */
+    /* on-chip batches of more instances than CUs: level-search kernel, pack
+     * kernel, full kernel for the instances the pack kernel leaves
+     * (sw_kernels.hip) — the split buys several instances per CU; up to one
+     * instance per CU (a scheduler's single solve) the full kernel alone is
+     * one launch instead of three, and otherwise the full kernel for every
+     * instance */
 #ifdef SW_STAMPS
     const bool split = false; /* diagnostic builds time the phases inside the full kernel */
 #else
-    const bool split = one;
+    const bool split = one && B.count > kSplitMinCount;
 #endif
     hipError_t e = split ? sw_launch_split(&B, h->stream) : sw_launch_plan(&B, B.KT, one, lds, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");

@@ -205,12 +205,36 @@ __device__ __forceinline__ int32_t wave_sort_asc_i32(int32_t v) {
 
 /* Fixed halving tree over the wave (p[i] += p[i+h], h = 32 … 1); the result
  * is valid in lane 0. */
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+
+/* The tree's first two levels exchange wave halves (permlane32_swap) and row
+ * pairs (permlane16_swap): in the lanes that carry on, the two results are
+ * p[i] and p[i+h] in some order, and their sum is p[i] + p[i+h] bit for bit
+ * (IEEE addition commutes).  The last four levels are DPP row_shl.  No lane
+ * address register, unlike a __shfl_down (ds_bpermute) tree, whose hoisted
+ * addresses the compiler keeps live or spills across a whole kernel. */
 __device__ __forceinline__ double wave_dettree(double x) {
-#pragma unroll
-    for (int h = 32; h >= 1; h >>= 1) {
-        double y = __shfl_down(x, h, 64);
-        x = x + y;
+    {
+        const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        x = __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
     }
+    {
+        const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        x = __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+    }
+    x = x + dpp_f64<0x108>(x); /* row_shl:8 */
+    x = x + dpp_f64<0x104>(x); /* row_shl:4 */
+    x = x + dpp_f64<0x102>(x); /* row_shl:2 */
+    x = x + dpp_f64<0x101>(x); /* row_shl:1 */
     return x;
 }
 

@@ -1664,7 +1664,8 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     const double P2 = c.blk.detsum(p2);
     const int64_t any_n = c.blk.sum(any_l); /* its barrier: every mask row is final */
     if (any_n == 0) status |= SW_STATUS_NO_PLANNED;
-    emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
+    /* the result record first: the reduction's values die before the plan
+     * bytes' loop instead of being spilled across it */
     if (threadIdx.x == 0) {
         sw_out_dev o;
         o.objective = lv.U - c.k * lv.M;
@@ -1676,6 +1677,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
         o.status = status;
         *out = o;
     }
+    emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
 }
 
 template <int KT, bool ONE>

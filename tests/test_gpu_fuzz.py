@@ -30,3 +30,21 @@ def test_gpu_fuzz_workspace_path_matches_twin(gpu_solver, twin):
     for i, (a, r) in enumerate(zip(probs, rb)):
         check_plan_valid(a, r)
         assert_same_result(r, twin.solve(a), f"seed {100_000 + i} N={a.N} G={a.G} T={a.T}")
+
+
+def test_gpu_fuzz_split_path_matches_twin(gpu_solver, twin):
+    """A batch of more instances than CUs with every instance on-chip (T ≤ 32,
+    N ≤ 1024) takes the split kernels (level search, pack, slow-path full
+    kernel); smaller batches and single solves take the full kernel alone.
+    Both must give the twin's results bit for bit."""
+    probs = []
+    s = 200_000
+    while len(probs) < 384:
+        a = fuzz_problem(s)
+        s += 1
+        if a.T <= 32:
+            probs.append(a)
+    rb = gpu_solver.solve_batch(probs)
+    for i, (a, r) in enumerate(zip(probs, rb)):
+        check_plan_valid(a, r)
+        assert_same_result(r, twin.solve(a), f"split-path case {i} N={a.N} G={a.G} T={a.T}")
