@@ -571,8 +571,13 @@ def boundary_legs(args, solver, batch, results, local):
     caller keeps its arrays); each timed call is the C entry point itself.
 
     * host_boundary_solves_per_s — sw_plan_solve_batch on the same instances:
-      validate + pack into pinned staging + H2D, the kernel, plans / counts /
-      results D2H and unpacked into the caller's arrays;
+      validate + pack into pinned staging + H2D, the kernels, plans / counts /
+      results D2H and unpacked into the caller's arrays (byte plans, the
+      reference's x[j][t]); large on-chip batches run as a chunk pipeline
+      (sw_api.hip solve_pipelined: copies of one chunk overlap the kernels of
+      the next, host staging / unpacking on up to 16 threads);
+    * host_boundary_masks_solves_per_s — the same call with the bit-packed
+      plan (sw_result.plan_masks: 8 bytes per job instead of T) and counts;
     * single_instance_ms — one sw_plan_solve per call (the scheduler's call
       pattern: host arrays in, plan out), averaged over repeated calls;
     * sustained_solves_per_s — device-resident launches back to back for ~2 s
@@ -595,6 +600,22 @@ def boundary_legs(args, solver, batch, results, local):
     assert all(np.array_equal(batch[i].plan, results[i]["plan"]) for i in range(0, n, 97))
     out["host_boundary_solves_per_s"] = reps * n / dt
     out["host_boundary_ms_per_batch"] = dt / reps * 1e3
+    masks = [np.zeros(a.N, dtype=np.uint64) for a in batch]
+    for i in range(n):
+        ress[i].plan = None
+        ress[i].plan_masks = masks[i].ctypes.data_as(C.POINTER(C.c_uint64))
+    assert lib.sw_plan_solve_batch(solver.h, n, probs, ress) >= 0
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rc = lib.sw_plan_solve_batch(solver.h, n, probs, ress)
+    dt = time.perf_counter() - t0
+    assert rc >= 0
+    bits = np.uint64(1) << np.arange(batch[0].T, dtype=np.uint64)
+    for i in range(0, n, 97):
+        want = (results[i]["plan"].astype(np.uint64) * bits[None, :]).sum(axis=1, dtype=np.uint64)
+        assert np.array_equal(masks[i], want)
+    out["host_boundary_masks_solves_per_s"] = reps * n / dt
+    out["host_boundary_masks_ms_per_batch"] = dt / reps * 1e3
     one = sn.Solver(device=local)
     a = batch[0]
     p1, r1 = a.c_problem(), a.c_result()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 1
+#define SW_ABI_VERSION 2
 
 /* Limits of this build. */
 #define SW_MAX_ROUNDS 64 /* future_rounds T (reference configs use 20 and 30) */
@@ -110,6 +110,12 @@ typedef struct sw_problem {
  *   p2_objective  Σ_{n_j>0} p_j·(Σ_t t·y_jt)/n_j                           shockwave.py:309-322
  *   bound         an upper bound on the aggregate P1 optimum (fractional-knapsack bound)
  *   iters         number of level/price evaluations the solver made
+ * plan_masks (optional, ABI 2) is the same plan bit-packed: one word per job,
+ * bit t = plan[j][t] — 8 bytes per job across the host boundary instead of
+ * future_rounds.  Any of plan / plan_masks / planned_rounds may be NULL; the
+ * batch entry points copy back only what some result of the batch asks for.
+ * The sharded entry points (sw_dist_*) write plan and planned_rounds only and
+ * reject a non-NULL plan_masks.
  */
 typedef struct sw_result {
     uint8_t* plan;
@@ -121,6 +127,7 @@ typedef struct sw_result {
     double bound;
     int32_t iters;
     int32_t status;
+    uint64_t* plan_masks;
 } sw_result;
 
 /* Handle creation.  max_* reserve device capacity; 0 picks defaults. */

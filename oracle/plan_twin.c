@@ -833,6 +833,12 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     res->status = status;
     if (res->plan && N > 0) memcpy(res->plan, yf, (size_t)N * T);
     if (res->planned_rounds && N > 0) memcpy(res->planned_rounds, nb, sizeof(int32_t) * (size_t)N);
+    if (res->plan_masks)
+        for (int32_t j = 0; j < N; ++j) {
+            uint64_t m = 0;
+            for (int32_t t = 0; t < T; ++t) m |= (uint64_t)(yf[(size_t)j * T + t] != 0) << t;
+            res->plan_masks[j] = m;
+        }
     free(P.jc); free(P.key); free(P.Tj); free(n); free(nb); free(l); free(tk);
     free(placed); free(placed2); free(tmp); free(y1); free(y2); free(ybest);
     return (status & SW_STATUS_P2_FALLBACK) ? SW_FALLBACK : SW_OK;

@@ -11,9 +11,14 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
+#include <atomic>
+#include <climits>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/shockwave_amd.h"
@@ -22,8 +27,20 @@
 #include "sw_handle.h"
 #include "sw_validate.h"
 
-/* batches above this many instances take the split kernels (MI355X: 256 CUs) */
-constexpr int kSplitMinCount = 256;
+/* On-chip batches above this many instances take the split kernels
+ * (SW_SPLIT_MIN overrides).  The split buys several instances per CU in the
+ * light phases, but an instance its pack kernel leaves is solved again from
+ * the start by the full kernel, and each of the four kernels waits for its
+ * slowest instance: with few instances per CU (a single solve, the 512-
+ * instance C5 sweep with its slow small-cluster instances) one full kernel
+ * is faster. */
+static int split_min_count() {
+    static const int v = [] {
+        const char* e = getenv("SW_SPLIT_MIN");
+        return e ? atoi(e) : 1024;
+    }();
+    return v;
+}
 
 #define SW_P2X_ARR_BYTES 24 /* sw_p2x_dev.h: exchange workspace bytes per job */
 
@@ -73,6 +90,7 @@ int collect_timing(sw_handle* h) {
 }
 
 constexpr size_t kEventPairs = 256;
+constexpr int kMaxChunks = 16; /* host-boundary pipeline */
 
 }  // namespace
 
@@ -139,6 +157,8 @@ void sw_destroy(sw_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->up) (void)hipStreamSynchronize(h->up);
+    if (h->dn) (void)hipStreamSynchronize(h->dn);
     sw_shard_release(h);
     sw_mmf_release(h);
     h->d_inst.release(); h->d_w.release(); h->d_F.release(); h->d_E.release();
@@ -148,6 +168,11 @@ void sw_destroy(sw_handle* h) {
     h->d_masks.release(); h->d_p2ws.release(); h->d_nb.release(); h->d_lvl.release();
     h->h_w.release(); h->h_F.release(); h->h_E.release(); h->h_planned.release();
     h->h_d.release(); h->h_R.release(); h->h_p.release(); h->h_plan.release(); h->h_out.release();
+    h->h_masks.release(); h->h_inst.release();
+    for (hipEvent_t ev : h->ev_chunk)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->up) (void)hipStreamDestroy(h->up);
+    if (h->dn) (void)hipStreamDestroy(h->dn);
     for (hipEvent_t ev : h->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : h->ev_p2x)
@@ -160,22 +185,81 @@ const char* sw_last_error(const sw_handle* h) { return h ? h->err.c_str() : "nul
 
 void* sw_stream(sw_handle* h) { return h ? (void*)h->stream : nullptr; }
 
-int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
-    if (!h) return SW_ERR_INVALID;
+}  // extern "C"
+
+namespace {
+
+/* Host threads for validation, staging and unpacking: one per ~64k jobs, at
+ * most 16 (a GPU's CPU share on the MI355X box; SW_HOST_THREADS overrides). */
+int host_threads(int64_t jobs) {
+    static const int cap = [] {
+        const char* e = getenv("SW_HOST_THREADS");
+        const int v = e ? atoi(e) : 0;
+        if (v > 0) return std::min(v, 256);
+        const unsigned hw = std::thread::hardware_concurrency();
+        return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+    }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>(cap, jobs / 65536));
+}
+
+int64_t jobs_of(const sw_handle* h, int32_t lo, int32_t hi) {
+    return hi > lo ? h->inst[hi - 1].job_off + h->inst[hi - 1].N - h->inst[lo].job_off : 0;
+}
+
+/* f(a, b) over nt contiguous sub-ranges of instances [lo, hi) holding about
+ * equal numbers of jobs; the calling thread takes the first.  A thread that
+ * cannot be started runs its range inline (no exception crosses the ABI). */
+template <class F>
+void par_instances(const sw_handle* h, int32_t lo, int32_t hi, F&& f) {
+    const int nt = std::min<int64_t>(host_threads(jobs_of(h, lo, hi)), hi - lo);
+    if (nt <= 1) {
+        if (hi > lo) f(lo, hi);
+        return;
+    }
+    const int64_t J0 = h->inst[lo].job_off, J = jobs_of(h, lo, hi);
+    std::vector<int32_t> cut(nt + 1);
+    cut[0] = lo;
+    cut[nt] = hi;
+    for (int t = 1; t < nt; ++t) {
+        const int64_t target = J0 + J * t / nt;
+        auto it = std::lower_bound(h->inst.begin() + lo, h->inst.begin() + hi, target,
+                                   [](const sw_inst_dev& d, int64_t v) { return d.job_off < v; });
+        cut[t] = std::max(cut[t - 1], (int32_t)(it - h->inst.begin()));
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int t = 1; t < nt; ++t) {
+        if (cut[t] >= cut[t + 1]) continue;
+        try {
+            th.emplace_back([&f, &cut, t] { f(cut[t], cut[t + 1]); });
+        } catch (...) {
+            f(cut[t], cut[t + 1]);
+        }
+    }
+    if (cut[0] < cut[1]) f(cut[0], cut[1]);
+    for (auto& x : th) x.join();
+}
+
+/* Sizes and offsets of a batch from the problems' headers, capacity for it,
+ * and no batch described until its upload completes. */
+int prepare_batch(sw_handle* h, int32_t count, const sw_problem* probs) {
     if (count < 0 || (count > 0 && !probs)) return fail(h, SW_ERR_INVALID, "bad batch");
     SW_HIP(h, hipSetDevice(h->device));
     int64_t J = 0, P = 0;
     int32_t maxN = 0, maxT = 1;
     for (int32_t i = 0; i < count; ++i) {
-        if (sw_validate_problem(&probs[i]) != 0)
+        const sw_problem& pr = probs[i];
+        if (pr.num_jobs < 0 || pr.future_rounds < 1 || pr.future_rounds > SW_MAX_ROUNDS)
             return fail(h, SW_ERR_INVALID, "invalid problem at index " + std::to_string(i));
-        J += probs[i].num_jobs;
-        P += (int64_t)probs[i].num_jobs * probs[i].future_rounds;
-        maxN = std::max(maxN, probs[i].num_jobs);
-        maxT = std::max(maxT, probs[i].future_rounds);
+        J += pr.num_jobs;
+        P += (int64_t)pr.num_jobs * pr.future_rounds;
+        maxN = std::max(maxN, pr.num_jobs);
+        maxT = std::max(maxT, pr.future_rounds);
     }
     /* wait for any run still using the buffers */
     SW_HIP(h, hipStreamSynchronize(h->stream));
+    if (h->up) SW_HIP(h, hipStreamSynchronize(h->up));
+    if (h->dn) SW_HIP(h, hipStreamSynchronize(h->dn));
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
     /* the previous batch is gone from here on: a reserve below frees the
      * old buffers before it allocates, so a failure must leave no batch
@@ -202,63 +286,319 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
         return fail(h, SW_ERR_HIP, "P2 exchange workspace allocation failed");
     if (h->h_w.reserve(Jz) || h->h_F.reserve(Jz) || h->h_E.reserve(Jz) || h->h_d.reserve(Jz) ||
         h->h_R.reserve(Jz) || h->h_p.reserve(Jz) || h->h_planned.reserve(Jz) ||
-        h->h_plan.reserve((size_t)std::max<int64_t>(P, 1)) ||
-        h->h_out.reserve(std::max(count, 1)))
+        h->h_masks.reserve(Jz) || h->h_plan.reserve((size_t)std::max<int64_t>(P, 1)) ||
+        h->h_out.reserve(std::max(count, 1)) || h->h_inst.reserve(std::max(count, 1)))
         return fail(h, SW_ERR_HIP, "pinned allocation failed");
     h->inst.resize(count);
     h->Ns.resize(count);
     h->Ts.resize(count);
     int64_t jo = 0, po = 0;
     for (int32_t i = 0; i < count; ++i) {
-        const sw_problem& pr = probs[i];
         sw_inst_dev& d = h->inst[i];
-        memset(&d, 0, sizeof(d));
-        d.N = pr.num_jobs;
-        d.T = pr.future_rounds;
-        d.G = pr.num_gpus;
-        d.nb = pr.num_bases;
+        d.N = probs[i].num_jobs;
+        d.T = probs[i].future_rounds;
         d.job_off = jo;
         d.plan_off = po;
-        d.delta = pr.round_duration;
-        d.k = pr.regularizer;
-        for (int b = 0; b < SW_BMAX; ++b) {
-            d.beta[b] = b < pr.num_bases ? pr.bases[b] : 0.0;
-            d.ell[b] = b < pr.num_bases ? pr.log_bases[b] : 0.0;
-        }
-        const size_t n = (size_t)pr.num_jobs;
-        if (n) {
-            memcpy(h->h_w.p + jo, pr.nworkers, n * sizeof(int32_t));
-            memcpy(h->h_F.p + jo, pr.completed_epochs, n * sizeof(int32_t));
-            memcpy(h->h_E.p + jo, pr.total_epochs, n * sizeof(int32_t));
-            memcpy(h->h_d.p + jo, pr.epoch_duration, n * sizeof(double));
-            memcpy(h->h_R.p + jo, pr.remaining_runtime, n * sizeof(double));
-            memcpy(h->h_p.p + jo, pr.priority, n * sizeof(double));
-        }
-        h->Ns[i] = pr.num_jobs;
-        h->Ts[i] = pr.future_rounds;
-        jo += pr.num_jobs;
-        po += (int64_t)pr.num_jobs * pr.future_rounds;
+        h->Ns[i] = d.N;
+        h->Ts[i] = d.T;
+        jo += d.N;
+        po += (int64_t)d.N * d.T;
     }
     h->maxN = maxN;
     h->maxT = maxT;
-    if (count > 0) {
-        hipStream_t s = h->stream;
-        SW_HIP(h, hipMemcpyAsync(h->d_inst.p, h->inst.data(), count * sizeof(sw_inst_dev),
-                                 hipMemcpyHostToDevice, s));
-        if (J > 0) {
-            SW_HIP(h, hipMemcpyAsync(h->d_w.p, h->h_w.p, J * 4, hipMemcpyHostToDevice, s));
-            SW_HIP(h, hipMemcpyAsync(h->d_F.p, h->h_F.p, J * 4, hipMemcpyHostToDevice, s));
-            SW_HIP(h, hipMemcpyAsync(h->d_E.p, h->h_E.p, J * 4, hipMemcpyHostToDevice, s));
-            SW_HIP(h, hipMemcpyAsync(h->d_d.p, h->h_d.p, J * 8, hipMemcpyHostToDevice, s));
-            SW_HIP(h, hipMemcpyAsync(h->d_R.p, h->h_R.p, J * 8, hipMemcpyHostToDevice, s));
-            SW_HIP(h, hipMemcpyAsync(h->d_p.p, h->h_p.p, J * 8, hipMemcpyHostToDevice, s));
+    h->pend_count = count;
+    h->pend_jobs = J;
+    h->pend_plan = P;
+    return SW_OK;
+}
+
+/* Every problem of [0, count) validated (sw_validate.h) before the handle's
+ * current batch is touched, in parallel over equal instance ranges; the
+ * error names the first invalid index. */
+int validate_all(sw_handle* h, const sw_problem* probs, int32_t count) {
+    if (count < 0 || (count > 0 && !probs)) return fail(h, SW_ERR_INVALID, "bad batch");
+    std::atomic<int32_t> bad{INT32_MAX};
+    auto check = [&](int32_t a, int32_t b) {
+        for (int32_t i = a; i < b; ++i)
+            if (sw_validate_problem(&probs[i]) != 0) {
+                int32_t cur = bad.load();
+                while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+                }
+                return;
+            }
+    };
+    /* the thread count from the first problem's size (headers unchecked yet) */
+    const int64_t n0 = count > 0 && probs[0].num_jobs > 0 ? probs[0].num_jobs : 1;
+    const int nt = (int)std::min<int64_t>(host_threads(n0 * count), count);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const int32_t a = (int32_t)((int64_t)count * t / nt), b = (int32_t)((int64_t)count * (t + 1) / nt);
+        try {
+            th.emplace_back([&check, a, b] { check(a, b); });
+        } catch (...) {
+            check(a, b);
         }
-        SW_HIP(h, hipStreamSynchronize(s));
     }
-    h->count = count;
-    h->total_jobs = J;
-    h->total_plan = P;
+    check(0, nt > 1 ? (int32_t)((int64_t)count / nt) : count);
+    for (auto& x : th) x.join();
+    if (bad.load() != INT32_MAX)
+        return fail(h, SW_ERR_INVALID, "invalid problem at index " + std::to_string(bad.load()));
+    return SW_OK;
+}
+
+/* Instances [lo, hi) into the pinned staging (validated problems). */
+void stage(sw_handle* h, const sw_problem* probs, int32_t lo, int32_t hi) {
+    par_instances(h, lo, hi, [&](int32_t a, int32_t b) {
+        for (int32_t i = a; i < b; ++i) {
+            const sw_problem& pr = probs[i];
+            sw_inst_dev& d = h->inst[i];
+            const int64_t jo = d.job_off, po = d.plan_off;
+            memset(&d, 0, sizeof(d));
+            d.N = pr.num_jobs;
+            d.T = pr.future_rounds;
+            d.G = pr.num_gpus;
+            d.nb = pr.num_bases;
+            d.job_off = jo;
+            d.plan_off = po;
+            d.delta = pr.round_duration;
+            d.k = pr.regularizer;
+            for (int b = 0; b < SW_BMAX; ++b) {
+                d.beta[b] = b < pr.num_bases ? pr.bases[b] : 0.0;
+                d.ell[b] = b < pr.num_bases ? pr.log_bases[b] : 0.0;
+            }
+            h->h_inst.p[i] = d;
+            const size_t n = (size_t)pr.num_jobs;
+            if (n) {
+                memcpy(h->h_w.p + jo, pr.nworkers, n * sizeof(int32_t));
+                memcpy(h->h_F.p + jo, pr.completed_epochs, n * sizeof(int32_t));
+                memcpy(h->h_E.p + jo, pr.total_epochs, n * sizeof(int32_t));
+                memcpy(h->h_d.p + jo, pr.epoch_duration, n * sizeof(double));
+                memcpy(h->h_R.p + jo, pr.remaining_runtime, n * sizeof(double));
+                memcpy(h->h_p.p + jo, pr.priority, n * sizeof(double));
+            }
+        }
+    });
+}
+
+/* H2D of instances [lo, hi) (their descriptors and job arrays) on s. */
+int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
+    if (hi <= lo) return SW_OK;
+    SW_HIP(h, hipMemcpyAsync(h->d_inst.p + lo, h->h_inst.p + lo, (size_t)(hi - lo) * sizeof(sw_inst_dev),
+                             hipMemcpyHostToDevice, s));
+    const int64_t j0 = h->inst[lo].job_off, nj = jobs_of(h, lo, hi);
+    if (nj > 0) {
+        SW_HIP(h, hipMemcpyAsync(h->d_w.p + j0, h->h_w.p + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_F.p + j0, h->h_F.p + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_E.p + j0, h->h_E.p + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_d.p + j0, h->h_d.p + j0, nj * 8, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_R.p + j0, h->h_R.p + j0, nj * 8, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_p.p + j0, h->h_p.p + j0, nj * 8, hipMemcpyHostToDevice, s));
+    }
+    return SW_OK;
+}
+
+/* The solve kernels for instances [lo, hi) of the loaded batch on s: the
+ * per-instance arrays offset to lo, the per-job ones global (each
+ * descriptor holds its global job and plan offsets). */
+int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
+    sw_batch_dev B;
+    memset(&B, 0, sizeof(B));
+    B.inst = h->d_inst.p + lo;
+    B.count = hi - lo;
+    B.KT = h->maxT <= 32 ? 32 : 64;
+    B.w = h->d_w.p;
+    B.d = h->d_d.p;
+    B.F = h->d_F.p;
+    B.E = h->d_E.p;
+    B.R = h->d_R.p;
+    B.p = h->d_p.p;
+    B.plan = h->d_plan.p;
+    B.planned = h->d_planned.p;
+    B.masks = h->d_masks.p;
+    B.out = h->d_out.p + lo;
+    B.nb = h->d_nb.p;
+    B.lvl = h->d_lvl.p + lo;
+#ifdef SW_STAMPS
+    B.stamps = h->d_stamps.p + (size_t)lo * SW_STAMP_SLOTS;
+#endif
+    const int one = h->maxN <= SW_LDS_JOBS && h->maxT <= 32;
+    if (!one) {
+        B.ws.u8 = h->d_ws_u8.p;
+        B.ws.u64 = h->d_ws_u64.p;
+        B.ws.sort = h->d_ws_sort.p;
+        B.ws.keys = h->d_ws_keys.p;
+        B.ws.jc = h->d_ws_jc.p;
+    }
+    const size_t lds = sw_plan_kernel_lds_bytes(one);
+    if (timed) {
+        if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
+        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], s));
+    }
+    /* on-chip batches of more instances than CUs: level-search kernel, pack
+     * kernel, full kernel for the instances the pack kernel leaves
+     * (sw_kernels.hip) — the split buys several instances per CU; up to one
+     * instance per CU (a scheduler's single solve) the full kernel alone is
+     * one launch instead of three, and otherwise the full kernel for every
+     * instance */
+#ifdef SW_STAMPS
+    const bool split = false; /* diagnostic builds time the phases inside the full kernel */
+#else
+    const bool split = one && B.count > split_min_count();
+#endif
+    hipError_t e = split ? sw_launch_split(&B, s) : sw_launch_plan(&B, B.KT, one, lds, s);
+    if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");
+    if (timed) {
+        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], s));
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], s));
+    }
+    /* the P2 exchange step (sw_p2x_kernel.hip) on the plan kernel's masks */
+    e = sw_launch_p2x(&B, h->maxN, h->maxT, h->d_p2ws.p, s);
+    if (e != hipSuccess) return hip_fail(h, e, "sw_p2x_kernel launch");
+    if (timed) {
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used + 1], s));
+        h->ev_used++;
+    }
+    return SW_OK;
+}
+
+/* Which outputs the caller asked for (any result of the batch). */
+struct Wants {
+    bool plan = false, masks = false, planned = false;
+};
+
+Wants wants_of(const sw_result* res, int32_t count) {
+    Wants w;
+    for (int32_t i = 0; i < count; ++i) {
+        w.plan |= res[i].plan != nullptr;
+        w.masks |= res[i].plan_masks != nullptr;
+        w.planned |= res[i].planned_rounds != nullptr;
+    }
+    return w;
+}
+
+/* D2H of instances [lo, hi)'s outputs on s. */
+int d2h(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, const Wants& w) {
+    if (hi <= lo) return SW_OK;
+    const int64_t j0 = h->inst[lo].job_off, nj = jobs_of(h, lo, hi);
+    const int64_t p0 = h->inst[lo].plan_off,
+                  np = h->inst[hi - 1].plan_off + (int64_t)h->inst[hi - 1].N * h->inst[hi - 1].T - p0;
+    if (w.plan && np > 0)
+        SW_HIP(h, hipMemcpyAsync(h->h_plan.p + p0, h->d_plan.p + p0, np, hipMemcpyDeviceToHost, s));
+    if (w.masks && nj > 0)
+        SW_HIP(h, hipMemcpyAsync(h->h_masks.p + j0, h->d_masks.p + j0, nj * 8, hipMemcpyDeviceToHost, s));
+    if (w.planned && nj > 0)
+        SW_HIP(h, hipMemcpyAsync(h->h_planned.p + j0, h->d_planned.p + j0, nj * 4, hipMemcpyDeviceToHost, s));
+    SW_HIP(h, hipMemcpyAsync(h->h_out.p + lo, h->d_out.p + lo, (size_t)(hi - lo) * sizeof(sw_out_dev),
+                             hipMemcpyDeviceToHost, s));
+    return SW_OK;
+}
+
+/* Staged outputs of instances [lo, hi) into the caller's results, in
+ * parallel; SW_FALLBACK when any kept P1's placement. */
+int unpack(sw_handle* h, sw_result* res, int32_t lo, int32_t hi) {
+    std::atomic<int> fb{0};
+    par_instances(h, lo, hi, [&](int32_t a, int32_t b) {
+        int f = 0;
+        for (int32_t i = a; i < b; ++i) {
+            const sw_inst_dev& d = h->inst[i];
+            const sw_out_dev& o = h->h_out.p[i];
+            sw_result& r = res[i];
+            if (r.plan && d.N > 0) memcpy(r.plan, h->h_plan.p + d.plan_off, (size_t)d.N * d.T);
+            if (r.plan_masks && d.N > 0) memcpy(r.plan_masks, h->h_masks.p + d.job_off, (size_t)d.N * 8);
+            if (r.planned_rounds && d.N > 0)
+                memcpy(r.planned_rounds, h->h_planned.p + d.job_off, (size_t)d.N * 4);
+            r.objective = o.objective;
+            r.utility = o.utility;
+            r.makespan = o.makespan;
+            r.p2_objective = o.p2_objective;
+            r.bound = o.bound;
+            r.iters = o.iters;
+            r.status = o.status;
+            f |= (o.status & SW_STATUS_P2_FALLBACK) != 0;
+        }
+        if (f) fb.store(1);
+    });
+    return fb.load() ? SW_FALLBACK : SW_OK;
+}
+
+void mark_loaded(sw_handle* h) {
+    h->count = h->pend_count;
+    h->total_jobs = h->pend_jobs;
+    h->total_plan = h->pend_plan;
     h->loaded = true;
+}
+
+/* Chunks of a host-boundary solve (SW_PIPELINE_CHUNKS overrides; 1 = none). */
+int pipeline_chunks(int32_t count) {
+    static const int req = [] {
+        const char* e = getenv("SW_PIPELINE_CHUNKS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? std::min(v, kMaxChunks) : 4;
+    }();
+    /* chunks of at least 2048 instances: each launch keeps every CU busy */
+    return std::max(1, std::min<int>(req, count / 2048));
+}
+
+/*
+ * sw_plan_solve_batch over host buffers as a pipeline of chunks of
+ * instances: the host stages chunk c+1 and unpacks chunk c−1 while chunk c
+ * is on the GPU; its H2D (stream up), kernels (the handle's stream) and D2H
+ * (stream dn) are ordered by events, so one chunk's copies overlap the
+ * neighbouring chunks' kernels.  Every problem is validated before any is
+ * solved (the unchunked call's contract).
+ */
+int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_result* res, int nch) {
+    if (!h->up) SW_HIP(h, hipStreamCreateWithFlags(&h->up, hipStreamNonBlocking));
+    if (!h->dn) SW_HIP(h, hipStreamCreateWithFlags(&h->dn, hipStreamNonBlocking));
+    if (h->ev_chunk.empty()) {
+        h->ev_chunk.assign(3 * kMaxChunks, nullptr);
+        for (auto& ev : h->ev_chunk) SW_HIP(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    const Wants w = wants_of(res, count);
+    std::vector<int32_t> cut(nch + 1);
+    for (int c = 0; c <= nch; ++c) cut[c] = (int32_t)((int64_t)count * c / nch);
+    int rc = SW_OK, err = SW_OK;
+    for (int c = 0; c < nch && err == SW_OK; ++c) {
+        hipEvent_t e_up = h->ev_chunk[3 * c], e_k = h->ev_chunk[3 * c + 1], e_dn = h->ev_chunk[3 * c + 2];
+        stage(h, probs, cut[c], cut[c + 1]);
+        if ((err = h2d(h, cut[c], cut[c + 1], h->up)) != SW_OK) break;
+        SW_HIP(h, hipEventRecord(e_up, h->up));
+        SW_HIP(h, hipStreamWaitEvent(h->stream, e_up, 0));
+        if ((err = launch(h, cut[c], cut[c + 1], h->stream, false)) != SW_OK) break;
+        SW_HIP(h, hipEventRecord(e_k, h->stream));
+        SW_HIP(h, hipStreamWaitEvent(h->dn, e_k, 0));
+        if ((err = d2h(h, cut[c], cut[c + 1], h->dn, w)) != SW_OK) break;
+        SW_HIP(h, hipEventRecord(e_dn, h->dn));
+        if (c > 0) {
+            SW_HIP(h, hipEventSynchronize(h->ev_chunk[3 * (c - 1) + 2]));
+            rc |= unpack(h, res, cut[c - 1], cut[c]);
+        }
+    }
+    if (err != SW_OK) { /* nothing may still use the buffers */
+        (void)hipStreamSynchronize(h->up);
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipStreamSynchronize(h->dn);
+        return err;
+    }
+    SW_HIP(h, hipEventSynchronize(h->ev_chunk[3 * (nch - 1) + 2]));
+    rc |= unpack(h, res, cut[nch - 1], cut[nch]);
+    mark_loaded(h);
+    return rc ? SW_FALLBACK : SW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* probs) {
+    if (!h) return SW_ERR_INVALID;
+    int rc = validate_all(h, probs, count);
+    if (rc != SW_OK) return rc;
+    if ((rc = prepare_batch(h, count, probs)) != SW_OK) return rc;
+    stage(h, probs, 0, count);
+    if ((rc = h2d(h, 0, count, h->stream)) != SW_OK) return rc;
+    SW_HIP(h, hipStreamSynchronize(h->stream));
+    mark_loaded(h);
 #ifdef SW_STAMPS
     if (h->d_stamps.reserve((size_t)std::max(count, 1) * SW_STAMP_SLOTS))
         return fail(h, SW_ERR_HIP, "stamp buffer allocation failed");
@@ -282,64 +622,7 @@ int sw_batch_run(sw_handle* h) {
     if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
     if (h->count <= 0) return SW_OK;
     SW_HIP(h, hipSetDevice(h->device));
-    sw_batch_dev B;
-    memset(&B, 0, sizeof(B));
-    B.inst = h->d_inst.p;
-    B.count = h->count;
-    B.KT = h->maxT <= 32 ? 32 : 64;
-    B.w = h->d_w.p;
-    B.d = h->d_d.p;
-    B.F = h->d_F.p;
-    B.E = h->d_E.p;
-    B.R = h->d_R.p;
-    B.p = h->d_p.p;
-    B.plan = h->d_plan.p;
-    B.planned = h->d_planned.p;
-    B.masks = h->d_masks.p;
-    B.out = h->d_out.p;
-    B.nb = h->d_nb.p;
-    B.lvl = h->d_lvl.p;
-#ifdef SW_STAMPS
-    B.stamps = h->d_stamps.p;
-#endif
-    const int one = h->maxN <= SW_LDS_JOBS && h->maxT <= 32;
-    if (!one) {
-        B.ws.u8 = h->d_ws_u8.p;
-        B.ws.u64 = h->d_ws_u64.p;
-        B.ws.sort = h->d_ws_sort.p;
-        B.ws.keys = h->d_ws_keys.p;
-        B.ws.jc = h->d_ws_jc.p;
-    }
-    const size_t lds = sw_plan_kernel_lds_bytes(one);
-    if (h->timing) {
-        if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
-        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], h->stream));
-    }
-    /* on-chip batches of more instances than CUs: level-search kernel, pack
-     * kernel, full kernel for the instances the pack kernel leaves
-     * (sw_kernels.hip) — the split buys several instances per CU; up to one
-     * instance per CU (a scheduler's single solve) the full kernel alone is
-     * one launch instead of three, and otherwise the full kernel for every
-     * instance */
-#ifdef SW_STAMPS
-    const bool split = false; /* diagnostic builds time the phases inside the full kernel */
-#else
-    const bool split = one && B.count > kSplitMinCount;
-#endif
-    hipError_t e = split ? sw_launch_split(&B, h->stream) : sw_launch_plan(&B, B.KT, one, lds, h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");
-    if (h->timing) {
-        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], h->stream));
-        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], h->stream));
-    }
-    /* the P2 exchange step (sw_p2x_kernel.hip) on the plan kernel's masks */
-    e = sw_launch_p2x(&B, h->maxN, h->maxT, h->d_p2ws.p, h->stream);
-    if (e != hipSuccess) return hip_fail(h, e, "sw_p2x_kernel launch");
-    if (h->timing) {
-        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used + 1], h->stream));
-        h->ev_used++;
-    }
-    return SW_OK;
+    return launch(h, 0, h->count, h->stream, h->timing);
 }
 
 int sw_batch_download(sw_handle* h, sw_result* res) {
@@ -347,40 +630,34 @@ int sw_batch_download(sw_handle* h, sw_result* res) {
     if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
     if (h->count > 0 && !res) return fail(h, SW_ERR_INVALID, "null result array");
     SW_HIP(h, hipSetDevice(h->device));
-    hipStream_t s = h->stream;
-    if (h->count > 0) {
-        if (h->total_plan > 0)
-            SW_HIP(h, hipMemcpyAsync(h->h_plan.p, h->d_plan.p, h->total_plan,
-                                     hipMemcpyDeviceToHost, s));
-        if (h->total_jobs > 0)
-            SW_HIP(h, hipMemcpyAsync(h->h_planned.p, h->d_planned.p, h->total_jobs * 4,
-                                     hipMemcpyDeviceToHost, s));
-        SW_HIP(h, hipMemcpyAsync(h->h_out.p, h->d_out.p, h->count * sizeof(sw_out_dev),
-                                 hipMemcpyDeviceToHost, s));
-    }
-    SW_HIP(h, hipStreamSynchronize(s));
+    int rc = d2h(h, 0, h->count, h->stream, wants_of(res, h->count));
+    if (rc != SW_OK) return rc;
+    SW_HIP(h, hipStreamSynchronize(h->stream));
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
-    int rc = SW_OK;
-    for (int32_t i = 0; i < h->count; ++i) {
-        const sw_inst_dev& d = h->inst[i];
-        const sw_out_dev& o = h->h_out.p[i];
-        sw_result& r = res[i];
-        if (r.plan && d.N > 0) memcpy(r.plan, h->h_plan.p + d.plan_off, (size_t)d.N * d.T);
-        if (r.planned_rounds && d.N > 0)
-            memcpy(r.planned_rounds, h->h_planned.p + d.job_off, (size_t)d.N * 4);
-        r.objective = o.objective;
-        r.utility = o.utility;
-        r.makespan = o.makespan;
-        r.p2_objective = o.p2_objective;
-        r.bound = o.bound;
-        r.iters = o.iters;
-        r.status = o.status;
-        if (o.status & SW_STATUS_P2_FALLBACK) rc = SW_FALLBACK;
-    }
-    return rc;
+    return unpack(h, res, 0, h->count);
 }
 
 int sw_plan_solve_batch(sw_handle* h, int32_t count, const sw_problem* probs, sw_result* res) {
+    if (!h) return SW_ERR_INVALID;
+    if (count > 0 && !res) return fail(h, SW_ERR_INVALID, "null result array");
+#ifndef SW_STAMPS
+    /* the chunk pipeline for large on-chip batches on the handle's own
+     * stream (a borrowed stream keeps every step on it) */
+    const int nch = h->own_stream && !h->timing ? pipeline_chunks(count) : 1;
+    if (nch > 1) {
+        int32_t maxN = 0, maxT = 0;
+        for (int32_t i = 0; i < count && probs; ++i) {
+            maxN = std::max(maxN, probs[i].num_jobs);
+            maxT = std::max(maxT, probs[i].future_rounds);
+        }
+        if (maxN <= SW_LDS_JOBS && maxT <= 32) {
+            int rc = validate_all(h, probs, count);
+            if (rc != SW_OK) return rc;
+            if ((rc = prepare_batch(h, count, probs)) != SW_OK) return rc;
+            return solve_pipelined(h, count, probs, res, nch);
+        }
+    }
+#endif
     int rc = sw_batch_upload(h, count, probs);
     if (rc < 0) return rc;
     rc = sw_batch_run(h);

@@ -89,6 +89,15 @@ struct sw_handle {
     HostBuf<double> h_d, h_R, h_p;
     HostBuf<uint8_t> h_plan;
     HostBuf<sw_out_dev> h_out;
+    HostBuf<uint64_t> h_masks;    /* bit-packed plans (sw_result.plan_masks) */
+    HostBuf<sw_inst_dev> h_inst;
+    /* host-boundary chunk pipeline (sw_plan_solve_batch): copy streams and
+     * per-chunk events, created on first use */
+    hipStream_t up = nullptr, dn = nullptr;
+    std::vector<hipEvent_t> ev_chunk;
+    /* the batch being uploaded (described once its upload completes) */
+    int32_t pend_count = 0;
+    int64_t pend_jobs = 0, pend_plan = 0;
     /* timing: one event pair per timed launch, collected lazily */
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;

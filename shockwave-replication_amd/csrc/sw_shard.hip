@@ -2031,11 +2031,13 @@ extern "C" {
 
 int sw_dist_plan_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
                        sw_result* res) {
+    if (h && res && res->plan_masks) return h->err = "plan_masks: batch entry points only", SW_ERR_INVALID;
     return dist_solve(h, local, job_offset, total_jobs, res, false);
 }
 
 int sw_dist_plan_solve_dev(sw_handle* h, const sw_problem* local, int64_t job_offset,
                            int64_t total_jobs, sw_result* res) {
+    if (h && res && res->plan_masks) return h->err = "plan_masks: batch entry points only", SW_ERR_INVALID;
     return dist_solve(h, local, job_offset, total_jobs, res, true);
 }
 

@@ -73,6 +73,7 @@ class SwResult(C.Structure):
         ("bound", C.c_double),
         ("iters", C.c_int32),
         ("status", C.c_int32),
+        ("plan_masks", C.POINTER(C.c_uint64)),
     ]
 
 
@@ -428,12 +429,27 @@ class Solver:
                          "sw_plan_solve")
         return result_dict(res, arrays, rc)
 
-    def solve_batch(self, batch: list) -> list:
+    def solve_batch(self, batch: list, masks: bool = False, plan: bool = True) -> list:
+        """sw_plan_solve_batch over host arrays.  masks=True also asks for the
+        bit-packed plan (sw_result.plan_masks, one uint64 per job, returned as
+        "plan_masks"); plan=False leaves the byte plan out (arrays.plan is not
+        written)."""
         probs = (SwProblem * len(batch))(*[a.c_problem() for a in batch])
         ress = (SwResult * len(batch))(*[a.c_result() for a in batch])
+        mk = []
+        for i, a in enumerate(batch):
+            if not plan:
+                ress[i].plan = None
+            if masks:
+                m = np.zeros(a.N, dtype=np.uint64)
+                ress[i].plan_masks = m.ctypes.data_as(C.POINTER(C.c_uint64))
+                mk.append(m)
         rc = self._check(self.lib.sw_plan_solve_batch(self.h, len(batch), probs, ress),
                          "sw_plan_solve_batch")
-        return [result_dict(ress[i], a, rc) for i, a in enumerate(batch)]
+        out = [result_dict(ress[i], a, rc) for i, a in enumerate(batch)]
+        for d, m in zip(out, mk):
+            d["plan_masks"] = m
+        return out
 
     # device-resident batch (bench)
     def upload(self, batch: list):

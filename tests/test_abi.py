@@ -34,13 +34,13 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_version():
     lib = sn.load()
-    assert lib.sw_abi_version() == 1
+    assert lib.sw_abi_version() == 2
 
 
 def test_structs_match_header_layout():
     # sizes of the C structs on x86-64 (pointers 8 B, natural alignment)
     assert ctypes.sizeof(sn.SwProblem) == 4 * 4 + 8 * 2 + 8 * 8
-    assert ctypes.sizeof(sn.SwResult) == 8 * 2 + 8 * 5 + 4 * 2
+    assert ctypes.sizeof(sn.SwResult) == 8 * 2 + 8 * 5 + 4 * 2 + 8
     assert ctypes.sizeof(sn.SwConfig) == 4 * 2 + 8 + 4 + 4 + 8
 
 

@@ -33,13 +33,13 @@ def test_gpu_fuzz_workspace_path_matches_twin(gpu_solver, twin):
 
 
 def test_gpu_fuzz_split_path_matches_twin(gpu_solver, twin):
-    """A batch of more instances than CUs with every instance on-chip (T ≤ 32,
+    """A batch of more than 1,024 instances with every instance on-chip (T ≤ 32,
     N ≤ 1024) takes the split kernels (level search, pack, slow-path full
     kernel); smaller batches and single solves take the full kernel alone.
     Both must give the twin's results bit for bit."""
     probs = []
     s = 200_000
-    while len(probs) < 384:
+    while len(probs) < 1100:
         a = fuzz_problem(s)
         s += 1
         if a.T <= 32:
