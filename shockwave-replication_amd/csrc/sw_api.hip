@@ -34,6 +34,10 @@
  * slowest instance: with few instances per CU (a single solve, the 512-
  * instance C5 sweep with its slow small-cluster instances) one full kernel
  * is faster. */
+/* on-chip batches up to this many instances (one per CU) fuse the exchange
+ * step into the full kernel */
+constexpr int kFuseMaxCount = 256;
+
 static int split_min_count() {
     static const int v = [] {
         const char* e = getenv("SW_SPLIT_MIN");
@@ -48,8 +52,8 @@ extern "C" size_t sw_plan_kernel_lds_bytes(int one);
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream);
 extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream);
-extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, unsigned char* ws,
-                                    hipStream_t stream);
+extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, hipStream_t stream);
+extern "C" size_t sw_p2x_kernel_lds_bytes(int maxN, int maxT);
 
 namespace {
 
@@ -429,31 +433,40 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
         B.ws.keys = h->d_ws_keys.p;
         B.ws.jc = h->d_ws_jc.p;
     }
-    const size_t lds = sw_plan_kernel_lds_bytes(one);
+    B.p2ws = h->d_p2ws.p;
+    size_t lds = sw_plan_kernel_lds_bytes(one);
     if (timed) {
         if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], s));
     }
-    /* on-chip batches of more instances than CUs: level-search kernel, pack
-     * kernel, full kernel for the instances the pack kernel leaves
-     * (sw_kernels.hip) — the split buys several instances per CU; up to one
-     * instance per CU (a scheduler's single solve) the full kernel alone is
-     * one launch instead of three, and otherwise the full kernel for every
-     * instance */
+    /* large on-chip batches: level-search kernel, pack kernel, full kernel
+     * for the instances the pack kernel leaves (sw_kernels.hip), then the
+     * exchange kernel; on-chip batches of at most one instance per CU: the
+     * full kernel with the exchange step fused at its end (one launch; each
+     * CU runs its instance's solve and exchange back to back, instead of
+     * every exchange waiting for the batch's slowest solve); otherwise the
+     * full kernel, then the exchange kernel (at two or more instances per
+     * CU the fused form would serialise a CU's exchanges behind its solves,
+     * where the exchange kernel runs four per CU: C5's 512 instances take
+     * 2.03 ms fused against 1.93 ms, profiles/r3w_c5_stages.json) */
 #ifdef SW_STAMPS
     const bool split = false; /* diagnostic builds time the phases inside the full kernel */
 #else
     const bool split = one && B.count > split_min_count();
 #endif
+    B.fuse_p2x = one && !split && B.count <= kFuseMaxCount;
+    if (B.fuse_p2x) lds = std::max(lds, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT));
     hipError_t e = split ? sw_launch_split(&B, s) : sw_launch_plan(&B, B.KT, one, lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");
     if (timed) {
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], s));
         SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], s));
     }
-    /* the P2 exchange step (sw_p2x_kernel.hip) on the plan kernel's masks */
-    e = sw_launch_p2x(&B, h->maxN, h->maxT, h->d_p2ws.p, s);
-    if (e != hipSuccess) return hip_fail(h, e, "sw_p2x_kernel launch");
+    /* the P2 exchange step (sw_p2x_kernel.hip) on the plan kernels' masks */
+    if (!B.fuse_p2x) {
+        e = sw_launch_p2x(&B, h->maxN, h->maxT, s);
+        if (e != hipSuccess) return hip_fail(h, e, "sw_p2x_kernel launch");
+    }
     if (timed) {
         SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used + 1], s));
         h->ev_used++;
@@ -541,10 +554,10 @@ int pipeline_chunks(int32_t count) {
 
 /*
  * sw_plan_solve_batch over host buffers as a pipeline of chunks of
- * instances: the host stages chunk c+1 and unpacks chunk c−1 while chunk c
- * is on the GPU; its H2D (stream up), kernels (the handle's stream) and D2H
- * (stream dn) are ordered by events, so one chunk's copies overlap the
- * neighbouring chunks' kernels.  Every problem is validated before any is
+ * instances: the host stages chunk c+1 while chunk c crosses PCIe, and
+ * unpacks chunk c while later chunks are on the GPU; each chunk's H2D
+ * (stream up), kernels (the handle's stream) and D2H (stream dn) are ordered
+ * by events, so one chunk's copies overlap the neighbouring chunks' kernels.  Every problem is validated before any is
  * solved (the unchunked call's contract).
  */
 int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_result* res, int nch) {
@@ -569,10 +582,6 @@ int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_res
         SW_HIP(h, hipStreamWaitEvent(h->dn, e_k, 0));
         if ((err = d2h(h, cut[c], cut[c + 1], h->dn, w)) != SW_OK) break;
         SW_HIP(h, hipEventRecord(e_dn, h->dn));
-        if (c > 0) {
-            SW_HIP(h, hipEventSynchronize(h->ev_chunk[3 * (c - 1) + 2]));
-            rc |= unpack(h, res, cut[c - 1], cut[c]);
-        }
     }
     if (err != SW_OK) { /* nothing may still use the buffers */
         (void)hipStreamSynchronize(h->up);
@@ -580,8 +589,13 @@ int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_res
         (void)hipStreamSynchronize(h->dn);
         return err;
     }
-    SW_HIP(h, hipEventSynchronize(h->ev_chunk[3 * (nch - 1) + 2]));
-    rc |= unpack(h, res, cut[nch - 1], cut[nch]);
+    /* every chunk is staged and queued before the first unpack, so the
+     * copy engine streams the H2D of all chunks back to back and no chunk's
+     * kernels wait for the host */
+    for (int c = 0; c < nch; ++c) {
+        SW_HIP(h, hipEventSynchronize(h->ev_chunk[3 * c + 2]));
+        rc |= unpack(h, res, cut[c], cut[c + 1]);
+    }
     mark_loaded(h);
     return rc ? SW_FALLBACK : SW_OK;
 }

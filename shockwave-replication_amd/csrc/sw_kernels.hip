@@ -35,6 +35,7 @@
 #include "sw_device.h"
 #include "sw_pack.h"
 #include "sw_repair.h"
+#include "sw_p2x_inst.h"
 
 namespace {
 
@@ -2072,6 +2073,17 @@ template <int KT, bool ONE>
 __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
     solve_instance<KT, ONE>(B, sw_smem, blockIdx.x);
+    if constexpr (ONE) {
+        /* one launch for the whole batch: the instance's P2 exchange step
+         * right after its emit, in the same workgroup and LDS (the solve's
+         * state is dead by now), so that one instance's exchange overlaps
+         * other instances' solves instead of waiting for the slowest solve
+         * of the batch (sw_p2x_inst.h) */
+        if (B.fuse_p2x) {
+            __syncthreads();
+            sw_p2x_instance(B, B.p2ws, sw_smem, blockIdx.x);
+        }
+    }
 }
 
 template <int KT>
@@ -2098,6 +2110,7 @@ extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream) {
     hipLaunchKernelGGL((sw_level_kernel<32>), grid, block, sw_level_lds_bytes(), stream, *B);
     hipLaunchKernelGGL(sw_pack_kernel, grid, block, sw_pack_lds_bytes(), stream, *B);
     B->only_slow = 1;
+    B->fuse_p2x = 0; /* sw_p2x_kernel follows for every instance */
     hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, sw_plan_lds_bytes(true), stream, *B);
     B->only_slow = 0;
     return hipGetLastError();

@@ -4,12 +4,14 @@
  * sequential specification oracle/p2x_twin.c.  Reference: the P2 MILP,
  * shockwave.py:281-328 (Gurobi at MIPGap 1e-3).
  *
- * One 512-thread workgroup per instance, launched after sw_plan_kernel on
- * the same stream: the plan kernel leaves every job's final round mask in
+ * One 512-thread workgroup per instance, launched after the plan stage on
+ * the same stream: the plan kernels leave every job's final round mask in
  * HBM (batch.masks); this kernel improves the masks of the instances whose
  * P2 placement placed every round, rewrites the plan bytes of the jobs that
- * moved and the P2 objective.  The step itself is sw_p2x_block
- * (sw_p2x_dev.h), which the sharded engine runs on its gathered placement.
+ * moved and the P2 objective (sw_p2x_inst.h).  A batch solved by the full
+ * plan kernel alone runs the same step at the end of that kernel instead.
+ * The step itself is sw_p2x_block (sw_p2x_dev.h), which the sharded engine
+ * runs on its gathered placement.
  * The step is latency-bound (a chain of small block phases), so the kernel is
  * lean (few VGPRs, ~50 KB LDS at 900 jobs × 30 rounds) and several instances
  * share a CU.
@@ -23,94 +25,13 @@
 #include "sw_device.h"
 #include "sw_p2x.h"
 #include "sw_p2x_dev.h"
+#include "sw_p2x_inst.h"
 
-/*
- * The batch kernel: instance blockIdx.x.  The per-job arrays live in the
- * workspace ws (SW_P2X_ARR_BYTES per job, L2-resident while the instance
- * runs) so that the LDS holds only the step's own state (~30 KB at 900 jobs ×
- * 30 rounds); at ≤ 80 VGPRs (6 waves per SIMD) three workgroups share a CU.
- */
-__global__ __launch_bounds__(SW_BLOCK, 8) void sw_p2x_kernel(sw_batch_dev B, unsigned char* ws, int maxA,
-                                                             int maxT) {
+/* The batch kernel: instance blockIdx.x.  At ≤ 64 VGPRs and ~34 KB of LDS
+ * four 512-thread workgroups share a CU. */
+__global__ __launch_bounds__(SW_BLOCK, 8) void sw_p2x_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int inst = blockIdx.x;
-    /* maxA (= the batch's largest N) bounds every instance's active jobs */
-    const sw_inst_dev* I = &B.inst[inst];
-    sw_out_dev* out = &B.out[inst];
-    const int N = I->N, T = I->T, G = I->G;
-    if (out->status & SW_STATUS_P2_FALLBACK) return; /* P1's x is kept as is (:325-326) */
-    const int64_t jo = I->job_off;
-    sw_p2x_lds* L = reinterpret_cast<sw_p2x_lds*>(smem);
-    unsigned char* var = smem + ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15);
-    sw_blk blk;
-    blk.X = &L->X;
-    blk.par = 0;
-    sw_p2x_arrays X;
-    (void)maxA;
-    (void)maxT;
-    {
-        unsigned char* base = ws + (size_t)SW_P2X_ARR_BYTES * jo;
-        const size_t n = (size_t)N;
-        X.cc = reinterpret_cast<double*>(base);
-        X.cm = reinterpret_cast<uint64_t*>(X.cc + n);
-        X.cw = reinterpret_cast<int32_t*>(X.cm + n);
-        X.cj = X.cw + n;
-    }
-    /* compaction in job order: thread l takes jobs [l·q, (l+1)·q) (the
-     * plan kernel's job split, so the P2 sum below has its lanes) */
-    const int q = (N + SW_BLOCK - 1) / SW_BLOCK;
-    const int j0 = threadIdx.x * q, j1 = min(j0 + q, N);
-    int act = 0;
-    for (int j = j0; j < j1; ++j) act += B.masks[jo + j] != 0ull;
-    int A;
-    const int a0 = blk.exscan(act, A);
-    if (A > SW_P2X_AMAX) return;
-    for (int j = j0, a = a0; j < j1; ++j) {
-        const uint64_t m = B.masks[jo + j];
-        if (!m) continue;
-        X.cw[a] = B.w[jo + j];
-        X.cj[a] = j;
-        X.cc[a] = B.p[jo + j] / (double)__popcll(m);
-        X.cm[a] = m;
-        ++a;
-    }
-    __syncthreads();
-#ifdef SW_STAMPS
-    uint64_t* sp = B.stamps ? B.stamps + (size_t)inst * SW_STAMP_SLOTS + 32 : nullptr;
-#else
-    uint64_t* sp = nullptr;
-#endif
-    const int nc = sw_p2x_block<SW_WAVES>(blk, L, var, X, A, T, G, sp);
-    if (nc == 0) return;
-    /* rewrite the moved jobs' plan bytes; the P2 objective of the final
-     * masks, summed like the plan kernel's emit */
-    uint8_t* plan = B.plan + I->plan_off;
-    double acc = 0.0;
-    for (int j = j0, a = a0; j < j1; ++j) {
-        const uint64_t m0 = B.masks[jo + j];
-        if (!m0) {
-            acc = acc + 0.0;
-            continue;
-        }
-        const uint64_t m = X.cm[a++];
-        if (m != m0) {
-            B.masks[jo + j] = m;
-            for (int t = 0; t < T; ++t) plan[(size_t)j * T + t] = (uint8_t)((m >> t) & 1ull);
-        }
-        const int cnt = __popcll(m);
-        const int64_t Ssum = (int64_t)__popcll(m & 0xAAAAAAAAAAAAAAAAull) +
-                             2 * (int64_t)__popcll(m & 0xCCCCCCCCCCCCCCCCull) +
-                             4 * (int64_t)__popcll(m & 0xF0F0F0F0F0F0F0F0ull) +
-                             8 * (int64_t)__popcll(m & 0xFF00FF00FF00FF00ull) +
-                             16 * (int64_t)__popcll(m & 0xFFFF0000FFFF0000ull) +
-                             32 * (int64_t)__popcll(m & 0xFFFFFFFF00000000ull);
-        acc = acc + ((double)Ssum / (double)cnt) * B.p[jo + j];
-    }
-    const double P2 = blk.detsum(acc);
-    if (threadIdx.x == 0) {
-        out->p2_objective = P2;
-        out->status |= SW_STATUS_P2_EXCHANGED;
-    }
+    sw_p2x_instance(B, B.p2ws, smem, blockIdx.x);
 }
 
 /* LDS bytes of the batch kernel for instances up to maxN jobs, maxT rounds. */
@@ -118,10 +39,9 @@ extern "C" size_t sw_p2x_kernel_lds_bytes(int maxN, int maxT) {
     return ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15) + sw_p2x_var_bytes(maxN, maxT);
 }
 
-extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, unsigned char* ws,
-                                    hipStream_t stream) {
+extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, hipStream_t stream) {
     const size_t lds = sw_p2x_kernel_lds_bytes(maxN, maxT);
     dim3 grid(B->count), block(SW_BLOCK);
-    hipLaunchKernelGGL(sw_p2x_kernel, grid, block, lds, stream, *B, ws, maxN, maxT);
+    hipLaunchKernelGGL(sw_p2x_kernel, grid, block, lds, stream, *B);
     return hipGetLastError();
 }

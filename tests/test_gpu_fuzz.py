@@ -32,14 +32,17 @@ def test_gpu_fuzz_workspace_path_matches_twin(gpu_solver, twin):
         assert_same_result(r, twin.solve(a), f"seed {100_000 + i} N={a.N} G={a.G} T={a.T}")
 
 
-def test_gpu_fuzz_split_path_matches_twin(gpu_solver, twin):
-    """A batch of more than 1,024 instances with every instance on-chip (T ≤ 32,
-    N ≤ 1024) takes the split kernels (level search, pack, slow-path full
-    kernel); smaller batches and single solves take the full kernel alone.
-    Both must give the twin's results bit for bit."""
+@pytest.mark.parametrize("count", [600, 1100])
+def test_gpu_fuzz_onchip_batch_paths_match_twin(count, gpu_solver, twin):
+    """On-chip batches (T ≤ 32, N ≤ 1024) take one of three launch forms by
+    size (sw_api.hip launch): up to 256 instances the full kernel with the
+    exchange step fused (every single solve and small batch in this suite);
+    600 here: the full kernel, then sw_p2x_kernel; more than 1,024 (1,100
+    here): the split kernels (level search, pack, slow-path full kernel),
+    then sw_p2x_kernel.  All must give the twin's results bit for bit."""
     probs = []
     s = 200_000
-    while len(probs) < 1100:
+    while len(probs) < count:
         a = fuzz_problem(s)
         s += 1
         if a.T <= 32:
@@ -47,4 +50,4 @@ def test_gpu_fuzz_split_path_matches_twin(gpu_solver, twin):
     rb = gpu_solver.solve_batch(probs)
     for i, (a, r) in enumerate(zip(probs, rb)):
         check_plan_valid(a, r)
-        assert_same_result(r, twin.solve(a), f"split-path case {i} N={a.N} G={a.G} T={a.T}")
+        assert_same_result(r, twin.solve(a), f"{count}-batch case {i} N={a.N} G={a.G} T={a.T}")

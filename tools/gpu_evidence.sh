@@ -2,7 +2,8 @@
 # Evidence set for one build, one call: GPU parity suite, smoke, the
 # default bench line, rocprofv3 kernel stats of the C3 bench (no legs) and of
 # the C4 line, PMC passes at the default batch, phase stamps, the peer-transport
-# C4 timing at W = 2 / 4 as processes on one GPU.
+# C4 timing at W = 2 / 4 as processes on one GPU, the host-boundary timing
+# (tools/boundary.py) and the C5 sweep's stage times (tools/c5_stages.py).
 #   gpurun --timeout 1200 -- bash tools/gpu_evidence.sh <tag>
 set -o pipefail
 TAG=${1:-evidence}
@@ -18,7 +19,9 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 bash tools/pmc_c3.sh $TAG/pmc $B &&
 timeout -k 10 200 python -u tools/stamps.py 256 > $OUT/stamps.log 2>&1 &&
 timeout -k 10 200 python -u tools/peer_timing.py 2 100 > $OUT/peer_w2.json 2> $OUT/peer_w2.err &&
-timeout -k 10 200 python -u tools/peer_timing.py 4 100 > $OUT/peer_w4.json 2> $OUT/peer_w4.err
+timeout -k 10 200 python -u tools/peer_timing.py 4 100 > $OUT/peer_w4.json 2> $OUT/peer_w4.err &&
+timeout -k 10 120 python -u tools/boundary.py > $OUT/boundary.json 2> $OUT/boundary.err &&
+timeout -k 10 120 python -u tools/c5_stages.py > $OUT/c5_stages.json 2> $OUT/c5_stages.err
 rc=$?
 echo "exit $rc"; tail -2 $OUT/pytest_gpu.log; tail -1 $OUT/smoke.log; cat $OUT/bench.json; head -14 $OUT/stamps.log
 exit $rc
