@@ -2,6 +2,12 @@
 the twin's, with the fields that differ; batched and single solves.
 
     python tools/fuzz_scan.py [n_instances] [--single]
+    python tools/fuzz_scan.py n_instances --onchip CHUNK   # T <= 32 only, CHUNK per batch
+
+With --onchip every instance is on-chip (N <= 1024, T <= 32), so the launch
+form follows the chunk size (sw_api.hip launch): <= 256 the full kernel with
+the exchange step fused, 257..1024 the full kernel then sw_p2x_kernel, > 1024
+the split kernels then sw_p2x_kernel.
 """
 import ctypes
 import os
@@ -82,20 +88,29 @@ def main():
         return ablate([int(x) for x in sys.argv[2].split(",")])
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     single = "--single" in sys.argv
+    chunk = int(sys.argv[sys.argv.index("--onchip") + 1]) if "--onchip" in sys.argv else 512
+    seeds = list(range(n))
+    if "--onchip" in sys.argv:
+        seeds, s0 = [], 0
+        while len(seeds) < n:
+            if fz.fuzz_problem(s0).T <= 32:
+                seeds.append(s0)
+            s0 += 1
     s = sn.Solver(device=0)
     bad = 0
-    for c0 in range(0, n, 512):
-        probs = [fz.fuzz_problem(i) for i in range(c0, min(n, c0 + 512))]
+    for c0 in range(0, n, chunk):
+        probs = [fz.fuzz_problem(i) for i in seeds[c0:c0 + chunk]]
         rb = [s.solve(a) for a in probs] if single else s.solve_batch(probs)
         for i, (a, r) in enumerate(zip(probs, rb)):
             d = diff(r, twin(a))
             if d:
                 bad += 1
-                print(f"seed {c0 + i} N={a.N} G={a.G} T={a.T} k={a.k:g} nb={len(a.bases)} "
+                print(f"seed {seeds[c0 + i]} N={a.N} G={a.G} T={a.T} k={a.k:g} nb={len(a.bases)} "
                       f"wmax={a.w.max()}: " + "; ".join(d), flush=True)
-        if (c0 + 512) % 4096 == 0:
-            print(f"... {c0 + 512} solved, {bad} differ", flush=True)
-    print(f"{bad} of {n} differ ({'single' if single else 'batched'})", flush=True)
+        if (c0 // chunk + 1) % max(1, 4096 // chunk) == 0:
+            print(f"... {c0 + chunk} solved, {bad} differ", flush=True)
+    form = "single" if single else f"batched by {chunk}" + (" (on-chip)" if "--onchip" in sys.argv else "")
+    print(f"{bad} of {n} differ ({form})", flush=True)
     s.close()
 
 
