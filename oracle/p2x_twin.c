@@ -76,30 +76,13 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
  * lowest round whose predecessor walk never ends).  Returns its length and
  * its nodes from the lowest one in predecessor order (cyc[i+1] =
  * pred(cyc[i])) when its cost is negative, else 0. */
-#ifdef P2X_DEBUG
-#include <stdio.h>
-static long dbg_it, dbg_bf, dbg_walk, dbg_evals_cached, dbg_evals_full;
-static uint64_t dbg_dirty[SW_P2X_KMAX];
-static long dbg_len[8];
-static double dbg_pot[SW_TMAX + 1];
-static int dbg_pot_ok;
-static double dbg_potF[SW_P2X_KMAX][SW_TMAX + 1];
-static int dbg_potF_ok[SW_P2X_KMAX];
-static long dbg_skippable, dbg_cert;
-#endif
 static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
-#ifdef P2X_DEBUG
-    dbg_bf++;
-#endif
     const int32_t T = X->T;
     double d[SW_TMAX + 1], nd[SW_TMAX + 1];
     int32_t pr[SW_TMAX + 1], np[SW_TMAX + 1];
     for (int32_t x = 0; x <= T; ++x) { d[x] = 0.0; pr[x] = -1; }
     for (int32_t it = 0; it <= T; ++it) {
         int changed = 0;
-#ifdef P2X_DEBUG
-        dbg_it++;
-#endif
         for (int32_t u = 0; u < T; ++u) {
             double best = d[u];
             int32_t bp = pr[u];
@@ -124,10 +107,6 @@ static int32_t find_cycle(const p2x_t* X, int32_t F, int32_t* cyc) {
             changed |= best < d[T];
         }
         if (!changed) {
-#ifdef P2X_DEBUG
-            for (int32_t x = 0; x <= T; ++x) dbg_pot[x] = d[x];
-            dbg_pot_ok = 1;
-#endif
             return 0;
         }
         for (int32_t x = 0; x <= T; ++x) { d[x] = nd[x]; pr[x] = np[x]; }
@@ -257,9 +236,6 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
             v[q] = X->pc[q] * (double)S;
         }
     const double delta = sw_p2x_delta(twin_detsum(v, A), T, A);
-#ifdef P2X_DEBUG
-    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
-#endif
     int32_t cyc[SW_TMAX + 1];
     int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * 2 * (size_t)SW_P2X_MAX_MOVES);
     int32_t ncancel = 0;
@@ -269,45 +245,7 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
             const int32_t F = X->wc[ki];
             while (ncancel < SW_P2X_MAX_CANCEL) {
                 build_w(X, F, delta);
-#ifdef P2X_DEBUG
-                {   /* what a per-F cached W would recompute: rows/cols dirty since its last build */
-                    int32_t ncls = 0;
-                    for (int32_t k = 0; k < X->K; ++k) ncls += (X->wc[k] <= F && F % X->wc[k] == 0);
-                    const uint64_t dm = dbg_dirty[ki];
-                    long ent = 0;
-                    for (int32_t t = 0; t < T; ++t) for (int32_t u = 0; u < T; ++u)
-                        if (t != u && (((dm >> t) | (dm >> u)) & 1ull)) ++ent;
-                    dbg_evals_cached += ent * ncls;
-                    dbg_evals_full += (long)T * (T - 1) * ncls;
-                    dbg_dirty[ki] = 0;
-                }
-#endif
-#ifdef P2X_DEBUG
-                int skippable = 0;
-                if (dbg_potF_ok[ki]) { /* would the stored potential certify "no negative cycle"? */
-                    const double* P = dbg_potF[ki];
-                    skippable = 1;
-                    for (int32_t t = 0; t < T && skippable; ++t) {
-                        for (int32_t u = 0; u < T; ++u) {
-                            const double w = X->W[t * T + u];
-                            if (t != u && w < SW_P2X_NONE && w + P[t] - P[u] < 0.0) { skippable = 0; break; }
-                        }
-                        if (X->room[t] >= F && P[t] - P[T] < 0.0) skippable = 0; /* t -> V */
-                        if (P[T] - P[t] < 0.0) skippable = 0;                    /* V -> t */
-                    }
-                }
-                dbg_pot_ok = 0;
-#endif
                 const int32_t len = find_cycle(X, F, cyc);
-#ifdef P2X_DEBUG
-                if (len == 0) {
-                    dbg_cert++;
-                    dbg_skippable += skippable;
-                    if (dbg_pot_ok) { for (int32_t x = 0; x <= T; ++x) dbg_potF[ki][x] = dbg_pot[x]; dbg_potF_ok[ki] = 1; }
-                } else {
-                    dbg_potF_ok[ki] = 0;
-                }
-#endif
                 if (len == 0) break;
                 int32_t moves = 0; /* the cycle's job moves */
                 for (int32_t i = 0; i < len; ++i) {
@@ -316,33 +254,11 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
                 }
                 if (moves > SW_P2X_MAX_MOVES) break;
                 cancel(X, F, cyc, len, tmp);
-#ifdef P2X_DEBUG
-                {
-                    int32_t real = 0, hasv = 0;
-                    for (int32_t i = 0; i < len; ++i) { if (cyc[i] == T) hasv = 1; }
-                    real = len - hasv;
-                    dbg_len[real < 8 ? real : 7]++;
-                }
-                for (int32_t i = 0; i < len; ++i) {
-                    const int32_t u = cyc[i], t = cyc[(i + 1) % len];
-                    if (u < T && t < T) for (int32_t q2 = 0; q2 < SW_P2X_KMAX; ++q2) dbg_dirty[q2] |= (1ull << t) | (1ull << u);
-                }
-#endif
                 ++ncancel;
                 changed = 1;
             }
         }
     }
-#ifdef P2X_DEBUG
-    fprintf(stderr, "p2x A=%d K=%d cancels=%d bf=%ld iters=%ld evals_full=%ld evals_cached=%ld len2=%ld len3=%ld len4+=%ld\n", A, X->K,
-            ncancel, dbg_bf, dbg_it, dbg_evals_full, dbg_evals_cached, dbg_len[2], dbg_len[3], dbg_len[4]+dbg_len[5]+dbg_len[6]+dbg_len[7]);
-    for (int32_t k = 0; k < 8; ++k) dbg_len[k] = 0;
-    fprintf(stderr, "    certifications=%ld skippable=%ld\n", dbg_cert, dbg_skippable);
-    dbg_cert = dbg_skippable = 0;
-    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_potF_ok[k] = 0;
-    dbg_bf = dbg_it = dbg_evals_full = dbg_evals_cached = 0;
-    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) dbg_dirty[k] = ~0ull;
-#endif
     /* back to the input order */
     for (int32_t q = 0; q < A; ++q) {
         int32_t lo = 0, hi = A - 1;

@@ -40,11 +40,7 @@
 
 #include "sw_arith.h"
 
-#ifdef SW_P2X_EPS_OVERRIDE /* experiments only */
-#define SW_P2X_EPS SW_P2X_EPS_OVERRIDE
-#else
 #define SW_P2X_EPS 2e-4        /* δ = ε·P2₀/T per edge                          */
-#endif
 #define SW_P2X_MAX_CANCEL 256  /* cancels per solve                              */
 #define SW_P2X_QMAX 4          /* jobs one edge moves (F / w_k ≤ this): a w8 job
                                   against four w2 or two w4 jobs, not eight w1 —
