@@ -931,7 +931,7 @@ struct Ctx {
             for (int jj = kk >> 1; jj > 0; jj >>= 1) {
                 uint64_t ph, pl = 0;
                 if (jj >= 64) {
-                    uint64_t* xh = x + (size_t)buf * 2 * SW_BLOCK;
+                    uint64_t* xh = x + (size_t)buf * (TWO ? 2 : 1) * SW_BLOCK;
                     uint64_t* xl = xh + SW_BLOCK;
                     xh[e] = hi;
                     if (TWO) xl[e] = lo;
@@ -1066,6 +1066,9 @@ struct Ctx {
                  * SW_BLOCK of them one per thread (half the network of the
                  * 1024-slot sort), and thread t owns position t, so every pass
                  * of the round loop walks one position instead of E */
+                /* the pack kernel (SMALL) sorts ratio orders only (modes 4
+                 * and 5): one word per position, and its LDS holds
+                 * 3·SW_BLOCK words here (four instances per CU) */
                 uint64_t* xh = sbuf;
                 uint64_t* xl = sbuf + SW_BLOCK;
                 int b = abase;
@@ -1073,15 +1076,20 @@ struct Ctx {
                 for (int s = 0; s < E; ++s)
                     if (klo[s] != 0) {
                         xh[b] = khi[s];
-                        xl[b] = klo[s];
+                        if constexpr (!SMALL) xl[b] = klo[s];
                         ++b;
                     }
                 __syncthreads();
                 const bool mine = (int)threadIdx.x < A_;
                 uint64_t h1 = mine ? xh[threadIdx.x] : 0ull;
-                uint64_t l1 = mine ? xl[threadIdx.x] : 0ull;
-                if (ratio) sort_one<false>(h1, l1, sbuf + 2 * SW_BLOCK);
-                else sort_one<true>(h1, l1, sbuf + 2 * SW_BLOCK);
+                uint64_t l1 = 0ull;
+                if constexpr (SMALL) {
+                    sort_one<false>(h1, l1, sbuf + SW_BLOCK);
+                } else {
+                    l1 = mine ? xl[threadIdx.x] : 0ull;
+                    if (ratio) sort_one<false>(h1, l1, sbuf + 2 * SW_BLOCK);
+                    else sort_one<true>(h1, l1, sbuf + 2 * SW_BLOCK);
+                }
 #ifdef SW_STAMPS
                 if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
 #endif
@@ -1414,7 +1422,7 @@ __host__ __device__ constexpr size_t sw_pack_lds_bytes() {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     const size_t NJ = SW_LDS_JOBS;
     return r16(sizeof(sw_xchg)) + r16(sizeof(sw_pack_lds)) + r16(sizeof(int64_t) * 8) +
-           r16(sizeof(sw_repair_t)) + 3 * r16(NJ) + 2 * r16(8 * NJ) + r16(8 * 6 * SW_BLOCK);
+           r16(sizeof(sw_repair_t)) + 3 * r16(NJ) + 2 * r16(8 * NJ) + r16(8 * 3 * SW_BLOCK);
 }
 
 /*
@@ -1599,7 +1607,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.ybest = nullptr;
-    c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 6 * SW_BLOCK); /* compaction + sort_one exchange */
+    c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 3 * SW_BLOCK); /* compaction + sort_one exchange */
     c.pst = nullptr;
     c.pord = nullptr;
     c.pmask = nullptr;
@@ -2092,8 +2100,8 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_level_kernel(sw_batch_dev B) {
     level_instance<KT>(B, sw_smem, blockIdx.x);
 }
 
-/* ≤ 80 VGPRs: three 512-thread workgroups per CU (LDS ~47 KB each) */
-__global__ __launch_bounds__(SW_BLOCK, 6) void sw_pack_kernel(sw_batch_dev B) {
+/* ≤ 64 VGPRs, ~35 KB of LDS: four 512-thread workgroups per CU */
+__global__ __launch_bounds__(SW_BLOCK, 8) void sw_pack_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
     pack_instance(B, sw_smem, blockIdx.x);
 }
