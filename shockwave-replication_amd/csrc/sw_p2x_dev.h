@@ -393,7 +393,53 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     /* ---- positions: (class asc, sw_p2x_ckey(c) desc, job asc) by a bitonic
      *      sort in LDS over the next power of two (the bitset / W area is
      *      free until the first build) ---- */
-    {
+    if (A <= NT) {
+        /* one position per thread: (class, key) and (job << 32 | a), a
+         * bitonic network over the next power of two np with shuffles for
+         * strides < 64 and an LDS exchange above (16·np bytes, what the
+         * LDS sort below uses; jobs are distinct, so the order is the same) */
+        int np = 1;
+        while (np < A) np <<= 1;
+        uint64_t hi = ~0ull, lo = ~0ull;
+        if (tid < A) {
+            const uint64_t ck = sw_p2x_ckey(X.cc[tid]);
+            hi = ((uint64_t)p2x_class(L, X.cw[tid]) << 61) | (~ck & ((1ull << 61) - 1));
+            lo = ((uint64_t)(uint32_t)X.cj[tid] << 32) | (uint32_t)tid;
+        }
+        uint64_t* xs = reinterpret_cast<uint64_t*>(vb); /* [hi, lo][np] */
+        for (int kk = 2; kk <= np; kk <<= 1) {
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                uint64_t ph = ~0ull, pl = ~0ull;
+                if (jj >= 64) {
+                    if (tid < np) {
+                        xs[tid] = hi;
+                        xs[np + tid] = lo;
+                    }
+                    __syncthreads();
+                    if (tid < np) {
+                        ph = xs[tid ^ jj];
+                        pl = xs[np + (tid ^ jj)];
+                    }
+                    __syncthreads();
+                } else {
+                    ph = __shfl_xor(hi, jj, 64);
+                    pl = __shfl_xor(lo, jj, 64);
+                }
+                const bool up = (tid & kk) == 0, lower = (tid & jj) == 0;
+                const bool gt = hi > ph || (hi == ph && lo > pl);
+                if ((lower == up) ? gt : !gt) {
+                    hi = ph;
+                    lo = pl;
+                }
+            }
+        }
+        if (tid < A) {
+            const int a = (int)(uint32_t)lo;
+            ord[tid] = a;
+            pc[tid] = X.cc[a];
+        }
+        __syncthreads(); /* the sort scratch is read before the bitsets overwrite it */
+    } else {
         int np = 1;
         while (np < A) np <<= 1;
         uint64_t* k1 = reinterpret_cast<uint64_t*>(vb);
@@ -436,18 +482,36 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
         __syncthreads(); /* the sort scratch is read before the bitsets clear it */
     }
     P2X_STAMP(1);
-    /* ---- rank bitsets, free capacity, δ ---- */
-    for (int i = tid; i < nwords; i += NT) B[i] = 0ull;
-    if (tid < T) L->room[tid] = G;
-    __syncthreads();
-    for (int p = tid; p < A; p += NT) {
-        int k = 0;
-        while (p >= L->off[k + 1]) ++k;
-        const int r = p - L->off[k];
-        for (uint64_t m = X.cm[ord[p]]; m; m &= m - 1) {
-            const int t = __builtin_ctzll(m);
-            atomicOr((unsigned long long*)&B[L->boff[k] + t * L->nw[k] + (r >> 6)], 1ull << (r & 63));
-            atomicAdd(&L->room[t], -L->wc[k]);
+    /* ---- rank bitsets, free capacity, δ ----
+     * One wave per 64-rank word slot (class k, word w): lane r loads the
+     * mask of rank 64·w + r and each round's word is a ballot, written once
+     * (no clearing, no atomics: the per-position LDS atomics of 64 ranks into
+     * one word, and of every position into T room counters, serialised). */
+    {
+        const int lane = lane_id(), wv = wave_id();
+        int nslot = 0;
+        for (int k = 0; k < K; ++k) nslot += L->nw[k];
+        for (int sl = wv; sl < nslot; sl += NW) {
+            int k = 0, w = sl;
+            while (w >= L->nw[k]) w -= L->nw[k++];
+            const int r = 64 * w + lane;
+            const uint64_t m = r < L->M[k] ? X.cm[ord[L->off[k] + r]] : 0ull;
+            uint64_t* Bk = B + L->boff[k] + w;
+            for (int t = 0; t < T; ++t) {
+                const uint64_t word = __ballot((m >> t) & 1ull);
+                if (lane == 0) Bk[t * L->nw[k]] = word;
+            }
+        }
+        __syncthreads();
+        if (tid < T) { /* G minus the round's width: Σ_k w_k · members of class k in t */
+            int32_t used = 0;
+            for (int k = 0; k < K; ++k) {
+                const uint64_t* Bk = B + L->boff[k] + tid * L->nw[k];
+                int32_t c = 0;
+                for (int w = 0; w < L->nw[k]; ++w) c += __popcll(Bk[w]);
+                used += c * L->wc[k];
+            }
+            L->room[tid] = G - used;
         }
     }
     {

@@ -27,10 +27,12 @@ def main():
     lib = sn.load(path)
     lib.sw_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     cases = {
-        "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] != "-v" else 64)],
+        "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64)],
         "g64_900x20_k1e-3": [ss.synth_problem(i, 900, 64, 20, 120.0, 1e-3, 15.0) for i in range(16)],
         "g128_120x20_k10": [ss.synth_problem(i, 120, 128, 20, 120.0, 10.0, 5.0) for i in range(16)],
     }
+    if "--c4" in sys.argv:  # the C4 instance alone (workspace path; its exchange at 10k jobs)
+        cases = {"c4_10000x30": [ss.synth_problem(77, 10000, 2848, 30, 120.0, 1e5, 5.0)]}
     names = ["setup", "p1_level_search", "p1_pack", "p1_misc", "p2_pack", "emit"]
     for name, batch in cases.items():
         s = sn.Solver(device=0, lib=lib)
