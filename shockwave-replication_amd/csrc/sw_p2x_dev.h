@@ -299,11 +299,7 @@ static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const ui
                 if (q == 0) continue;
                 const int nw = L->nw[k];
                 const uint64_t* Bk = B + L->boff[k];
-#ifdef P2X_EXPERIMENT_TRIVIAL_COST
-                const double cost = (double)(u - t) * pc[L->off[k]] + (double)(Bk[t * nw] & 7);
-#else
                 const double cost = p2x_cost_dev(Bk + t * nw, Bk + u * nw, nw, q, t, u, pc + L->off[k]);
-#endif
                 if (cost < best) {
                     best = cost;
                     bk = k;
@@ -334,7 +330,81 @@ static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const ui
     } while (0)
 #endif
 
-template <int NW>
+/* Bitonic sort of np = E·NT (class/key, job << 32 | a) pairs, E per thread
+ * in registers (thread tid holds entries tid·E … tid·E + E − 1): strides
+ * below E inside the thread, below 64·E by shuffles, larger ones through
+ * the LDS exchange xs (16·np bytes).  Entries past A are (~0, ~0). */
+template <int NT, int EMAX>
+static __device__ __forceinline__ void p2x_sort_regs(uint64_t (&hi)[EMAX], uint64_t (&lo)[EMAX], int E,
+                                                     int np, uint64_t* xs) {
+    const int tid = threadIdx.x;
+    for (int kk = 2; kk <= np; kk <<= 1) {
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            if (jj < E) { /* both entries in this thread */
+#pragma unroll
+                for (int e = 0; e < EMAX; ++e) {
+                    const int f = e ^ jj;
+                    if (e < E && f > e) {
+                        const int i = tid * E + e;
+                        const bool up = (i & kk) == 0;
+                        uint64_t ah = hi[e], al = lo[e], bh = 0, bl = 0;
+#pragma unroll
+                        for (int g = 0; g < EMAX; ++g)
+                            if (g == f) { bh = hi[g]; bl = lo[g]; }
+                        const bool gt = ah > bh || (ah == bh && al > bl);
+                        if (up == gt) { /* swap */
+                            hi[e] = bh; lo[e] = bl;
+#pragma unroll
+                            for (int g = 0; g < EMAX; ++g)
+                                if (g == f) { hi[g] = ah; lo[g] = al; }
+                        }
+                    }
+                }
+            } else {
+                uint64_t ph[EMAX], pl[EMAX];
+                const int dj = jj / E; /* partner thread tid ^ dj, same slot */
+                if (dj < 64) {
+#pragma unroll
+                    for (int e = 0; e < EMAX; ++e) {
+                        ph[e] = __shfl_xor(hi[e], dj, 64);
+                        pl[e] = __shfl_xor(lo[e], dj, 64);
+                    }
+                } else {
+                    if (tid * E < np)
+                        for (int e = 0; e < E; ++e) {
+                            xs[tid * E + e] = hi[e];
+                            xs[np + tid * E + e] = lo[e];
+                        }
+                    __syncthreads();
+                    const int pt = tid ^ dj;
+                    if (tid * E < np)
+                        for (int e = 0; e < E; ++e) {
+                            ph[e] = xs[pt * E + e];
+                            pl[e] = xs[np + pt * E + e];
+                        }
+                    __syncthreads();
+                }
+                const bool lower = (tid & dj) == 0;
+#pragma unroll
+                for (int e = 0; e < EMAX; ++e) {
+                    if (e >= E) continue;
+                    const int i = tid * E + e;
+                    const bool up = (i & kk) == 0;
+                    const bool gt = hi[e] > ph[e] || (hi[e] == ph[e] && lo[e] > pl[e]);
+                    if ((lower == up) ? gt : !gt) {
+                        hi[e] = ph[e];
+                        lo[e] = pl[e];
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* EMAX: entries per thread the rank sort may hold in registers (the sharded
+ * engine's single-workgroup step, up to SW_P2X_AMAX positions, uses 8; the
+ * batch kernel, capped at 64 VGPRs, 1 and an LDS network above 512) */
+template <int NW, int EMAX = 1>
 __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, unsigned char* var,
                                             const sw_p2x_arrays& X, int A, int T, int G,
                                             uint64_t* sp = nullptr) {
@@ -439,6 +509,33 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             pc[tid] = X.cc[a];
         }
         __syncthreads(); /* the sort scratch is read before the bitsets overwrite it */
+    } else if (EMAX > 1 && A <= EMAX * NT) {
+        int np = 1;
+        while (np < A) np <<= 1;
+        const int E = np / NT; /* A > NT: np ≥ 2·NT */
+        uint64_t hi[EMAX], lo[EMAX];
+#pragma unroll
+        for (int e = 0; e < EMAX; ++e) {
+            const int i = tid * E + e;
+            hi[e] = ~0ull;
+            lo[e] = ~0ull;
+            if (e < E && i < A) {
+                const uint64_t ck = sw_p2x_ckey(X.cc[i]);
+                hi[e] = ((uint64_t)p2x_class(L, X.cw[i]) << 61) | (~ck & ((1ull << 61) - 1));
+                lo[e] = ((uint64_t)(uint32_t)X.cj[i] << 32) | (uint32_t)i;
+            }
+        }
+        p2x_sort_regs<NT, EMAX>(hi, lo, E, np, reinterpret_cast<uint64_t*>(vb));
+#pragma unroll
+        for (int e = 0; e < EMAX; ++e) {
+            const int p = tid * E + e;
+            if (e < E && p < A) {
+                const int a = (int)(uint32_t)lo[e];
+                ord[p] = a;
+                pc[p] = X.cc[a];
+            }
+        }
+        __syncthreads(); /* the sort scratch is read before the bitsets overwrite it */
     } else {
         int np = 1;
         while (np < A) np <<= 1;
@@ -458,10 +555,18 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             }
         }
         __syncthreads();
+        /* strides below a wave's chunk (np / NW entries, aligned) pair entries
+         * of the same chunk: that wave runs those stages alone, with wave-level
+         * ordering instead of block barriers */
+        const int chunk = np / NW;
+        const int lane = lane_id(), wv = wave_id();
         for (int k = 2; k <= np; k <<= 1) {
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int x = tid; x < (np >> 1); x += NT) {
-                    const int i = 2 * x - (x & (j - 1)), l = i + j;
+                const bool local = j < chunk;
+                const int x0 = local ? lane : tid, xs = local ? 64 : NT;
+                const int nx = local ? (chunk >> 1) : (np >> 1), base = local ? wv * chunk : 0;
+                for (int x = x0; x < nx; x += xs) {
+                    const int i = base + 2 * x - (x & (j - 1)), l = i + j;
                     const uint64_t a1 = k1[i], b1 = k1[l];
                     const uint32_t a2 = k2[i], b2 = k2[l];
                     const bool gt = a1 > b1 || (a1 == b1 && a2 > b2);
@@ -471,7 +576,12 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                         const uint32_t t = ka[i]; ka[i] = ka[l]; ka[l] = t;
                     }
                 }
-                __syncthreads();
+                /* the next stage may pair across chunks: a block barrier
+                 * unless it stays inside this wave's chunk */
+                const int nj = j > 1 ? (j >> 1) : k; /* the next stage's stride (k doubles) */
+                const bool next_local = (j > 1 || (k << 1) <= np) && nj < chunk;
+                if (local && next_local) wave_sync();
+                else __syncthreads();
             }
         }
         for (int p = tid; p < A; p += NT) {

@@ -879,7 +879,7 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all
         ++a;
     }
     __syncthreads();
-    const int nc = sw_p2x_block<SW_WAVES>(blk, L, var, X, A, S.T, S.G);
+    const int nc = sw_p2x_block<SW_WAVES, 8>(blk, L, var, X, A, S.T, S.G);
     if (nc > 0)
         for (int i = threadIdx.x; i < A; i += SW_BLOCK) {
             const int64_t j = X.cj[i];
