@@ -81,3 +81,27 @@ def test_gpu_pipelined_invalid_problem_names_index_and_keeps_batch(gpu_solver):
     after = gpu_solver.download()
     for b, c in zip(before, after):
         assert_same_result(b, c, "batch kept")
+
+
+def test_gpu_pipelined_batch_with_empty_instances_and_no_outputs(gpu_solver, twin):
+    """Empty instances (no jobs) anywhere in a pipelined batch, chunk
+    boundaries included, and a call that asks for no per-job outputs at all
+    (plan = plan_masks = planned_rounds = NULL): every result field still
+    matches the twin."""
+    import ctypes
+
+    import sw_native as sn
+    import sw_synth as ss
+
+    probs = onchip(4608, 340_000)
+    for i in list(range(0, 4608, 97)) + [2303, 2304, 4607]:
+        probs[i] = ss.synth_problem(i, 0, 16, 10, 120.0, 1.0, 5.0)
+    rb = gpu_solver.solve_batch(probs)
+    for i in range(0, 4608, 7):
+        assert_same_result(rb[i], twin.solve(probs[i]), f"case {i} N={probs[i].N}")
+    cp = (sn.SwProblem * len(probs))(*[a.c_problem() for a in probs])
+    cr = (sn.SwResult * len(probs))()
+    assert gpu_solver.lib.sw_plan_solve_batch(gpu_solver.h, len(probs), cp, cr) >= 0
+    for i in range(0, 4608, 7):
+        assert cr[i].objective == rb[i]["objective"] and cr[i].status == rb[i]["status"], i
+        assert cr[i].p2_objective == rb[i]["p2_objective"], i
