@@ -96,6 +96,37 @@ int collect_timing(sw_handle* h) {
 constexpr size_t kEventPairs = 256;
 constexpr int kMaxChunks = 16; /* host-boundary pipeline */
 
+size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
+
+/* The input block of J jobs: w, F, E (int32) then d, R, p (f64). */
+size_t in_block_bytes(int64_t J) { return 3 * a16((size_t)J * 4) + 3 * a16((size_t)J * 8); }
+
+/* The output block: count results, J counts, P plan bytes. */
+size_t res_block_bytes(int32_t count, int64_t J, int64_t P) {
+    return a16((size_t)count * sizeof(sw_out_dev)) + a16((size_t)J * 4) + a16((size_t)P);
+}
+
+/* Views of both blocks (device and pinned) for a batch of count instances,
+ * J jobs and P plan bytes; the blocks are reserved for at least these. */
+void set_views(sw_handle* h, int32_t count, int64_t J, int64_t P) {
+    const size_t i4 = a16((size_t)J * 4), i8 = a16((size_t)J * 8);
+    unsigned char* d = h->d_in.p;
+    unsigned char* x = h->h_in.p;
+    h->d_w = (int32_t*)d;            h->h_w = (int32_t*)x;
+    h->d_F = (int32_t*)(d + i4);     h->h_F = (int32_t*)(x + i4);
+    h->d_E = (int32_t*)(d + 2 * i4); h->h_E = (int32_t*)(x + 2 * i4);
+    h->d_d = (double*)(d + 3 * i4);  h->h_d = (double*)(x + 3 * i4);
+    h->d_R = (double*)(d + 3 * i4 + i8);     h->h_R = (double*)(x + 3 * i4 + i8);
+    h->d_p = (double*)(d + 3 * i4 + 2 * i8); h->h_p = (double*)(x + 3 * i4 + 2 * i8);
+    h->in_bytes = in_block_bytes(J);
+    const size_t o = a16((size_t)count * sizeof(sw_out_dev)), c = a16((size_t)J * 4);
+    h->d_out = (sw_out_dev*)h->d_res.p;          h->h_out = (sw_out_dev*)h->h_res.p;
+    h->d_planned = (int32_t*)(h->d_res.p + o);   h->h_planned = (int32_t*)(h->h_res.p + o);
+    h->d_plan = h->d_res.p + o + c;              h->h_plan = h->h_res.p + o + c;
+    h->res_bytes = res_block_bytes(count, J, P);
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -145,10 +176,9 @@ sw_handle* sw_create(const sw_config* cfg) {
     /* optional up-front reservation */
     if (cfg && cfg->max_instances > 0 && cfg->max_total_jobs > 0) {
         size_t J = (size_t)cfg->max_total_jobs, I = (size_t)cfg->max_instances;
-        if (h->d_inst.reserve(I) || h->d_out.reserve(I) || h->d_w.reserve(J) ||
-            h->d_F.reserve(J) || h->d_E.reserve(J) || h->d_planned.reserve(J) || h->d_masks.reserve(J) ||
-            h->d_d.reserve(J) || h->d_R.reserve(J) || h->d_p.reserve(J) ||
-            h->d_plan.reserve(J * SW_MAX_ROUNDS)) {
+        if (h->d_inst.reserve(I) || h->d_in.reserve(in_block_bytes((int64_t)J)) ||
+            h->d_res.reserve(res_block_bytes((int32_t)I, (int64_t)J, (int64_t)J * SW_MAX_ROUNDS)) ||
+            h->d_masks.reserve(J)) {
             g_create_error = "device reservation failed";
             sw_destroy(h);
             return nullptr;
@@ -165,13 +195,11 @@ void sw_destroy(sw_handle* h) {
     if (h->dn) (void)hipStreamSynchronize(h->dn);
     sw_shard_release(h);
     sw_mmf_release(h);
-    h->d_inst.release(); h->d_w.release(); h->d_F.release(); h->d_E.release();
-    h->d_planned.release(); h->d_d.release(); h->d_R.release(); h->d_p.release();
-    h->d_plan.release(); h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
-    h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_out.release(); h->d_stamps.release();
+    h->d_inst.release(); h->d_in.release(); h->d_res.release();
+    h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
+    h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_stamps.release();
     h->d_masks.release(); h->d_p2ws.release(); h->d_nb.release(); h->d_lvl.release();
-    h->h_w.release(); h->h_F.release(); h->h_E.release(); h->h_planned.release();
-    h->h_d.release(); h->h_R.release(); h->h_p.release(); h->h_plan.release(); h->h_out.release();
+    h->h_in.release(); h->h_res.release();
     h->h_masks.release(); h->h_inst.release();
     for (hipEvent_t ev : h->ev_chunk)
         if (ev) (void)hipEventDestroy(ev);
@@ -273,11 +301,9 @@ int prepare_batch(sw_handle* h, int32_t count, const sw_problem* probs) {
     h->total_jobs = 0;
     h->total_plan = 0;
     const size_t Jz = (size_t)std::max<int64_t>(J, 1);
-    if (h->d_inst.reserve(std::max(count, 1)) || h->d_out.reserve(std::max(count, 1)) ||
-        h->d_w.reserve(Jz) || h->d_F.reserve(Jz) || h->d_E.reserve(Jz) ||
-        h->d_planned.reserve(Jz) || h->d_d.reserve(Jz) || h->d_R.reserve(Jz) ||
-        h->d_p.reserve(Jz) || h->d_masks.reserve(Jz) || h->d_nb.reserve(Jz) ||
-        h->d_lvl.reserve(std::max(count, 1)) || h->d_plan.reserve((size_t)std::max<int64_t>(P, 1)))
+    const size_t inb = in_block_bytes((int64_t)Jz), resb = res_block_bytes(std::max(count, 1), (int64_t)Jz, std::max<int64_t>(P, 1));
+    if (h->d_inst.reserve(std::max(count, 1)) || h->d_in.reserve(inb) || h->d_res.reserve(resb) ||
+        h->d_masks.reserve(Jz) || h->d_nb.reserve(Jz) || h->d_lvl.reserve(std::max(count, 1)))
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS || maxT > 32) {
         const int KT = maxT <= 32 ? 32 : 64;
@@ -288,11 +314,10 @@ int prepare_batch(sw_handle* h, int32_t count, const sw_problem* probs) {
     }
     if (h->d_p2ws.reserve(Jz * SW_P2X_ARR_BYTES))
         return fail(h, SW_ERR_HIP, "P2 exchange workspace allocation failed");
-    if (h->h_w.reserve(Jz) || h->h_F.reserve(Jz) || h->h_E.reserve(Jz) || h->h_d.reserve(Jz) ||
-        h->h_R.reserve(Jz) || h->h_p.reserve(Jz) || h->h_planned.reserve(Jz) ||
-        h->h_masks.reserve(Jz) || h->h_plan.reserve((size_t)std::max<int64_t>(P, 1)) ||
-        h->h_out.reserve(std::max(count, 1)) || h->h_inst.reserve(std::max(count, 1)))
+    if (h->h_in.reserve(inb) || h->h_res.reserve(resb) || h->h_masks.reserve(Jz) ||
+        h->h_inst.reserve(std::max(count, 1)))
         return fail(h, SW_ERR_HIP, "pinned allocation failed");
+    set_views(h, std::max(count, 1), (int64_t)Jz, std::max<int64_t>(P, 1));
     h->inst.resize(count);
     h->Ns.resize(count);
     h->Ts.resize(count);
@@ -373,12 +398,12 @@ void stage(sw_handle* h, const sw_problem* probs, int32_t lo, int32_t hi) {
             h->h_inst.p[i] = d;
             const size_t n = (size_t)pr.num_jobs;
             if (n) {
-                memcpy(h->h_w.p + jo, pr.nworkers, n * sizeof(int32_t));
-                memcpy(h->h_F.p + jo, pr.completed_epochs, n * sizeof(int32_t));
-                memcpy(h->h_E.p + jo, pr.total_epochs, n * sizeof(int32_t));
-                memcpy(h->h_d.p + jo, pr.epoch_duration, n * sizeof(double));
-                memcpy(h->h_R.p + jo, pr.remaining_runtime, n * sizeof(double));
-                memcpy(h->h_p.p + jo, pr.priority, n * sizeof(double));
+                memcpy(h->h_w + jo, pr.nworkers, n * sizeof(int32_t));
+                memcpy(h->h_F + jo, pr.completed_epochs, n * sizeof(int32_t));
+                memcpy(h->h_E + jo, pr.total_epochs, n * sizeof(int32_t));
+                memcpy(h->h_d + jo, pr.epoch_duration, n * sizeof(double));
+                memcpy(h->h_R + jo, pr.remaining_runtime, n * sizeof(double));
+                memcpy(h->h_p + jo, pr.priority, n * sizeof(double));
             }
         }
     });
@@ -390,13 +415,15 @@ int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
     SW_HIP(h, hipMemcpyAsync(h->d_inst.p + lo, h->h_inst.p + lo, (size_t)(hi - lo) * sizeof(sw_inst_dev),
                              hipMemcpyHostToDevice, s));
     const int64_t j0 = h->inst[lo].job_off, nj = jobs_of(h, lo, hi);
-    if (nj > 0) {
-        SW_HIP(h, hipMemcpyAsync(h->d_w.p + j0, h->h_w.p + j0, nj * 4, hipMemcpyHostToDevice, s));
-        SW_HIP(h, hipMemcpyAsync(h->d_F.p + j0, h->h_F.p + j0, nj * 4, hipMemcpyHostToDevice, s));
-        SW_HIP(h, hipMemcpyAsync(h->d_E.p + j0, h->h_E.p + j0, nj * 4, hipMemcpyHostToDevice, s));
-        SW_HIP(h, hipMemcpyAsync(h->d_d.p + j0, h->h_d.p + j0, nj * 8, hipMemcpyHostToDevice, s));
-        SW_HIP(h, hipMemcpyAsync(h->d_R.p + j0, h->h_R.p + j0, nj * 8, hipMemcpyHostToDevice, s));
-        SW_HIP(h, hipMemcpyAsync(h->d_p.p + j0, h->h_p.p + j0, nj * 8, hipMemcpyHostToDevice, s));
+    if (nj > 0 && lo == 0 && hi == h->pend_count) { /* the whole batch: one copy of the block */
+        SW_HIP(h, hipMemcpyAsync(h->d_in.p, h->h_in.p, h->in_bytes, hipMemcpyHostToDevice, s));
+    } else if (nj > 0) {
+        SW_HIP(h, hipMemcpyAsync(h->d_w + j0, h->h_w + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_F + j0, h->h_F + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_E + j0, h->h_E + j0, nj * 4, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_d + j0, h->h_d + j0, nj * 8, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_R + j0, h->h_R + j0, nj * 8, hipMemcpyHostToDevice, s));
+        SW_HIP(h, hipMemcpyAsync(h->d_p + j0, h->h_p + j0, nj * 8, hipMemcpyHostToDevice, s));
     }
     return SW_OK;
 }
@@ -410,16 +437,16 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
     B.inst = h->d_inst.p + lo;
     B.count = hi - lo;
     B.KT = h->maxT <= 32 ? 32 : 64;
-    B.w = h->d_w.p;
-    B.d = h->d_d.p;
-    B.F = h->d_F.p;
-    B.E = h->d_E.p;
-    B.R = h->d_R.p;
-    B.p = h->d_p.p;
-    B.plan = h->d_plan.p;
-    B.planned = h->d_planned.p;
+    B.w = h->d_w;
+    B.d = h->d_d;
+    B.F = h->d_F;
+    B.E = h->d_E;
+    B.R = h->d_R;
+    B.p = h->d_p;
+    B.plan = h->d_plan;
+    B.planned = h->d_planned;
     B.masks = h->d_masks.p;
-    B.out = h->d_out.p + lo;
+    B.out = h->d_out + lo;
     B.nb = h->d_nb.p;
     B.lvl = h->d_lvl.p + lo;
 #ifdef SW_STAMPS
@@ -495,13 +522,17 @@ int d2h(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, const Wants& w) {
     const int64_t j0 = h->inst[lo].job_off, nj = jobs_of(h, lo, hi);
     const int64_t p0 = h->inst[lo].plan_off,
                   np = h->inst[hi - 1].plan_off + (int64_t)h->inst[hi - 1].N * h->inst[hi - 1].T - p0;
-    if (w.plan && np > 0)
-        SW_HIP(h, hipMemcpyAsync(h->h_plan.p + p0, h->d_plan.p + p0, np, hipMemcpyDeviceToHost, s));
     if (w.masks && nj > 0)
         SW_HIP(h, hipMemcpyAsync(h->h_masks.p + j0, h->d_masks.p + j0, nj * 8, hipMemcpyDeviceToHost, s));
+    if (lo == 0 && hi == h->pend_count && w.plan && w.planned) { /* results, counts, plans: one copy */
+        SW_HIP(h, hipMemcpyAsync(h->h_res.p, h->d_res.p, h->res_bytes, hipMemcpyDeviceToHost, s));
+        return SW_OK;
+    }
+    if (w.plan && np > 0)
+        SW_HIP(h, hipMemcpyAsync(h->h_plan + p0, h->d_plan + p0, np, hipMemcpyDeviceToHost, s));
     if (w.planned && nj > 0)
-        SW_HIP(h, hipMemcpyAsync(h->h_planned.p + j0, h->d_planned.p + j0, nj * 4, hipMemcpyDeviceToHost, s));
-    SW_HIP(h, hipMemcpyAsync(h->h_out.p + lo, h->d_out.p + lo, (size_t)(hi - lo) * sizeof(sw_out_dev),
+        SW_HIP(h, hipMemcpyAsync(h->h_planned + j0, h->d_planned + j0, nj * 4, hipMemcpyDeviceToHost, s));
+    SW_HIP(h, hipMemcpyAsync(h->h_out + lo, h->d_out + lo, (size_t)(hi - lo) * sizeof(sw_out_dev),
                              hipMemcpyDeviceToHost, s));
     return SW_OK;
 }
@@ -514,12 +545,12 @@ int unpack(sw_handle* h, sw_result* res, int32_t lo, int32_t hi) {
         int f = 0;
         for (int32_t i = a; i < b; ++i) {
             const sw_inst_dev& d = h->inst[i];
-            const sw_out_dev& o = h->h_out.p[i];
+            const sw_out_dev& o = h->h_out[i];
             sw_result& r = res[i];
-            if (r.plan && d.N > 0) memcpy(r.plan, h->h_plan.p + d.plan_off, (size_t)d.N * d.T);
+            if (r.plan && d.N > 0) memcpy(r.plan, h->h_plan + d.plan_off, (size_t)d.N * d.T);
             if (r.plan_masks && d.N > 0) memcpy(r.plan_masks, h->h_masks.p + d.job_off, (size_t)d.N * 8);
             if (r.planned_rounds && d.N > 0)
-                memcpy(r.planned_rounds, h->h_planned.p + d.job_off, (size_t)d.N * 4);
+                memcpy(r.planned_rounds, h->h_planned + d.job_off, (size_t)d.N * 4);
             r.objective = o.objective;
             r.utility = o.utility;
             r.makespan = o.makespan;

@@ -72,23 +72,30 @@ struct sw_handle {
     std::vector<int32_t> Ns, Ts;
     /* device */
     DevBuf<sw_inst_dev> d_inst;
-    DevBuf<int32_t> d_w, d_F, d_E, d_planned;
-    DevBuf<double> d_d, d_R, d_p;
-    DevBuf<uint8_t> d_plan, d_ws_u8;
+    /* the per-job inputs of a batch as one block (one H2D for a whole
+     * batch), and its outputs as another (one D2H): views set per batch by
+     * sw_api.hip set_views() */
+    DevBuf<unsigned char> d_in, d_res;
+    int32_t *d_w = nullptr, *d_F = nullptr, *d_E = nullptr, *d_planned = nullptr;
+    double *d_d = nullptr, *d_R = nullptr, *d_p = nullptr;
+    uint8_t* d_plan = nullptr;
+    sw_out_dev* d_out = nullptr;
+    size_t in_bytes = 0, res_bytes = 0; /* the current batch's block sizes */
+    DevBuf<uint8_t> d_ws_u8;
     DevBuf<uint64_t> d_ws_u64, d_ws_sort;
     DevBuf<float> d_ws_keys;
     DevBuf<sw_jobc> d_ws_jc;
-    DevBuf<sw_out_dev> d_out;
     DevBuf<uint64_t> d_masks;     /* final round masks (plan kernel → P2 exchange) */
     DevBuf<uint8_t> d_nb;         /* level-search counts (level kernel → pack kernel) */
     DevBuf<sw_lvl_dev> d_lvl;     /* level-search results per instance                */
     DevBuf<unsigned char> d_p2ws; /* P2 exchange arrays of instances > SW_LDS_JOBS jobs */
     DevBuf<uint64_t> d_stamps; /* SW_STAMPS diagnostic builds */
     /* pinned staging */
-    HostBuf<int32_t> h_w, h_F, h_E, h_planned;
-    HostBuf<double> h_d, h_R, h_p;
-    HostBuf<uint8_t> h_plan;
-    HostBuf<sw_out_dev> h_out;
+    HostBuf<unsigned char> h_in, h_res; /* the blocks' pinned mirrors */
+    int32_t *h_w = nullptr, *h_F = nullptr, *h_E = nullptr, *h_planned = nullptr;
+    double *h_d = nullptr, *h_R = nullptr, *h_p = nullptr;
+    uint8_t* h_plan = nullptr;
+    sw_out_dev* h_out = nullptr;
     HostBuf<uint64_t> h_masks;    /* bit-packed plans (sw_result.plan_masks) */
     HostBuf<sw_inst_dev> h_inst;
     /* host-boundary chunk pipeline (sw_plan_solve_batch): copy streams and
