@@ -98,8 +98,11 @@ constexpr int kMaxChunks = 16; /* host-boundary pipeline */
 
 size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
 
-/* The input block of J jobs: w, F, E (int32) then d, R, p (f64). */
-size_t in_block_bytes(int64_t J) { return 3 * a16((size_t)J * 4) + 3 * a16((size_t)J * 8); }
+/* The input block of count instances and J jobs: the descriptors, then w,
+ * F, E (int32) and d, R, p (f64). */
+size_t in_block_bytes(int32_t count, int64_t J) {
+    return a16((size_t)count * sizeof(sw_inst_dev)) + 3 * a16((size_t)J * 4) + 3 * a16((size_t)J * 8);
+}
 
 /* The output block: count results, J counts, P plan bytes. */
 size_t res_block_bytes(int32_t count, int64_t J, int64_t P) {
@@ -110,15 +113,18 @@ size_t res_block_bytes(int32_t count, int64_t J, int64_t P) {
  * J jobs and P plan bytes; the blocks are reserved for at least these. */
 void set_views(sw_handle* h, int32_t count, int64_t J, int64_t P) {
     const size_t i4 = a16((size_t)J * 4), i8 = a16((size_t)J * 8);
-    unsigned char* d = h->d_in.p;
-    unsigned char* x = h->h_in.p;
+    const size_t id = a16((size_t)count * sizeof(sw_inst_dev));
+    h->d_inst = (sw_inst_dev*)h->d_in.p;
+    h->h_inst = (sw_inst_dev*)h->h_in.p;
+    unsigned char* d = h->d_in.p + id;
+    unsigned char* x = h->h_in.p + id;
     h->d_w = (int32_t*)d;            h->h_w = (int32_t*)x;
     h->d_F = (int32_t*)(d + i4);     h->h_F = (int32_t*)(x + i4);
     h->d_E = (int32_t*)(d + 2 * i4); h->h_E = (int32_t*)(x + 2 * i4);
     h->d_d = (double*)(d + 3 * i4);  h->h_d = (double*)(x + 3 * i4);
     h->d_R = (double*)(d + 3 * i4 + i8);     h->h_R = (double*)(x + 3 * i4 + i8);
     h->d_p = (double*)(d + 3 * i4 + 2 * i8); h->h_p = (double*)(x + 3 * i4 + 2 * i8);
-    h->in_bytes = in_block_bytes(J);
+    h->in_bytes = in_block_bytes(count, J);
     const size_t o = a16((size_t)count * sizeof(sw_out_dev)), c = a16((size_t)J * 4);
     h->d_out = (sw_out_dev*)h->d_res.p;          h->h_out = (sw_out_dev*)h->h_res.p;
     h->d_planned = (int32_t*)(h->d_res.p + o);   h->h_planned = (int32_t*)(h->h_res.p + o);
@@ -176,7 +182,7 @@ sw_handle* sw_create(const sw_config* cfg) {
     /* optional up-front reservation */
     if (cfg && cfg->max_instances > 0 && cfg->max_total_jobs > 0) {
         size_t J = (size_t)cfg->max_total_jobs, I = (size_t)cfg->max_instances;
-        if (h->d_inst.reserve(I) || h->d_in.reserve(in_block_bytes((int64_t)J)) ||
+        if (h->d_in.reserve(in_block_bytes((int32_t)I, (int64_t)J)) ||
             h->d_res.reserve(res_block_bytes((int32_t)I, (int64_t)J, (int64_t)J * SW_MAX_ROUNDS)) ||
             h->d_masks.reserve(J)) {
             g_create_error = "device reservation failed";
@@ -195,12 +201,12 @@ void sw_destroy(sw_handle* h) {
     if (h->dn) (void)hipStreamSynchronize(h->dn);
     sw_shard_release(h);
     sw_mmf_release(h);
-    h->d_inst.release(); h->d_in.release(); h->d_res.release();
+    h->d_in.release(); h->d_res.release();
     h->d_ws_u8.release(); h->d_ws_u64.release(); h->d_ws_sort.release();
     h->d_ws_keys.release(); h->d_ws_jc.release(); h->d_stamps.release();
     h->d_masks.release(); h->d_p2ws.release(); h->d_nb.release(); h->d_lvl.release();
     h->h_in.release(); h->h_res.release();
-    h->h_masks.release(); h->h_inst.release();
+    h->h_masks.release();
     for (hipEvent_t ev : h->ev_chunk)
         if (ev) (void)hipEventDestroy(ev);
     if (h->up) (void)hipStreamDestroy(h->up);
@@ -301,8 +307,8 @@ int prepare_batch(sw_handle* h, int32_t count, const sw_problem* probs) {
     h->total_jobs = 0;
     h->total_plan = 0;
     const size_t Jz = (size_t)std::max<int64_t>(J, 1);
-    const size_t inb = in_block_bytes((int64_t)Jz), resb = res_block_bytes(std::max(count, 1), (int64_t)Jz, std::max<int64_t>(P, 1));
-    if (h->d_inst.reserve(std::max(count, 1)) || h->d_in.reserve(inb) || h->d_res.reserve(resb) ||
+    const size_t inb = in_block_bytes(std::max(count, 1), (int64_t)Jz), resb = res_block_bytes(std::max(count, 1), (int64_t)Jz, std::max<int64_t>(P, 1));
+    if (h->d_in.reserve(inb) || h->d_res.reserve(resb) ||
         h->d_masks.reserve(Jz) || h->d_nb.reserve(Jz) || h->d_lvl.reserve(std::max(count, 1)))
         return fail(h, SW_ERR_HIP, "device allocation failed");
     if (maxN > SW_LDS_JOBS || maxT > 32) {
@@ -314,8 +320,7 @@ int prepare_batch(sw_handle* h, int32_t count, const sw_problem* probs) {
     }
     if (h->d_p2ws.reserve(Jz * SW_P2X_ARR_BYTES))
         return fail(h, SW_ERR_HIP, "P2 exchange workspace allocation failed");
-    if (h->h_in.reserve(inb) || h->h_res.reserve(resb) || h->h_masks.reserve(Jz) ||
-        h->h_inst.reserve(std::max(count, 1)))
+    if (h->h_in.reserve(inb) || h->h_res.reserve(resb) || h->h_masks.reserve(Jz))
         return fail(h, SW_ERR_HIP, "pinned allocation failed");
     set_views(h, std::max(count, 1), (int64_t)Jz, std::max<int64_t>(P, 1));
     h->inst.resize(count);
@@ -395,7 +400,7 @@ void stage(sw_handle* h, const sw_problem* probs, int32_t lo, int32_t hi) {
                 d.beta[b] = b < pr.num_bases ? pr.bases[b] : 0.0;
                 d.ell[b] = b < pr.num_bases ? pr.log_bases[b] : 0.0;
             }
-            h->h_inst.p[i] = d;
+            h->h_inst[i] = d;
             const size_t n = (size_t)pr.num_jobs;
             if (n) {
                 memcpy(h->h_w + jo, pr.nworkers, n * sizeof(int32_t));
@@ -412,12 +417,14 @@ void stage(sw_handle* h, const sw_problem* probs, int32_t lo, int32_t hi) {
 /* H2D of instances [lo, hi) (their descriptors and job arrays) on s. */
 int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
     if (hi <= lo) return SW_OK;
-    SW_HIP(h, hipMemcpyAsync(h->d_inst.p + lo, h->h_inst.p + lo, (size_t)(hi - lo) * sizeof(sw_inst_dev),
-                             hipMemcpyHostToDevice, s));
     const int64_t j0 = h->inst[lo].job_off, nj = jobs_of(h, lo, hi);
-    if (nj > 0 && lo == 0 && hi == h->pend_count) { /* the whole batch: one copy of the block */
+    if (lo == 0 && hi == h->pend_count) { /* the whole batch: one copy of the block */
         SW_HIP(h, hipMemcpyAsync(h->d_in.p, h->h_in.p, h->in_bytes, hipMemcpyHostToDevice, s));
-    } else if (nj > 0) {
+        return SW_OK;
+    }
+    SW_HIP(h, hipMemcpyAsync(h->d_inst + lo, h->h_inst + lo, (size_t)(hi - lo) * sizeof(sw_inst_dev),
+                             hipMemcpyHostToDevice, s));
+    if (nj > 0) {
         SW_HIP(h, hipMemcpyAsync(h->d_w + j0, h->h_w + j0, nj * 4, hipMemcpyHostToDevice, s));
         SW_HIP(h, hipMemcpyAsync(h->d_F + j0, h->h_F + j0, nj * 4, hipMemcpyHostToDevice, s));
         SW_HIP(h, hipMemcpyAsync(h->d_E + j0, h->h_E + j0, nj * 4, hipMemcpyHostToDevice, s));
@@ -434,7 +441,7 @@ int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
 int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
     sw_batch_dev B;
     memset(&B, 0, sizeof(B));
-    B.inst = h->d_inst.p + lo;
+    B.inst = h->d_inst + lo;
     B.count = hi - lo;
     B.KT = h->maxT <= 32 ? 32 : 64;
     B.w = h->d_w;

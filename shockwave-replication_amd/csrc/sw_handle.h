@@ -71,7 +71,7 @@ struct sw_handle {
     std::vector<sw_inst_dev> inst;
     std::vector<int32_t> Ns, Ts;
     /* device */
-    DevBuf<sw_inst_dev> d_inst;
+    sw_inst_dev* d_inst = nullptr; /* view: the head of d_in */
     /* the per-job inputs of a batch as one block (one H2D for a whole
      * batch), and its outputs as another (one D2H): views set per batch by
      * sw_api.hip set_views() */
@@ -97,7 +97,7 @@ struct sw_handle {
     uint8_t* h_plan = nullptr;
     sw_out_dev* h_out = nullptr;
     HostBuf<uint64_t> h_masks;    /* bit-packed plans (sw_result.plan_masks) */
-    HostBuf<sw_inst_dev> h_inst;
+    sw_inst_dev* h_inst = nullptr; /* view: the head of h_in */
     /* host-boundary chunk pipeline (sw_plan_solve_batch): copy streams and
      * per-chunk events, created on first use */
     hipStream_t up = nullptr, dn = nullptr;
