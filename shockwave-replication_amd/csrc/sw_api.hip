@@ -25,7 +25,12 @@
 #include "sw_arith.h"
 #include "sw_device.h"
 #include "sw_handle.h"
+#include "sw_p2x.h"
 #include "sw_validate.h"
+
+/* on-chip batches up to this many instances (one per CU) fuse the exchange
+ * step into the full kernel */
+constexpr int kFuseMaxCount = 256;
 
 /* On-chip batches above this many instances take the split kernels
  * (SW_SPLIT_MIN overrides).  The split buys several instances per CU in the
@@ -34,10 +39,6 @@
  * slowest instance: with few instances per CU (a single solve, the 512-
  * instance C5 sweep with its slow small-cluster instances) one full kernel
  * is faster. */
-/* on-chip batches up to this many instances (one per CU) fuse the exchange
- * step into the full kernel */
-constexpr int kFuseMaxCount = 256;
-
 static int split_min_count() {
     static const int v = [] {
         const char* e = getenv("SW_SPLIT_MIN");
@@ -46,7 +47,6 @@ static int split_min_count() {
     return v;
 }
 
-#define SW_P2X_ARR_BYTES 24 /* sw_p2x_dev.h: exchange workspace bytes per job */
 
 extern "C" size_t sw_plan_kernel_lds_bytes(int one);
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
@@ -184,7 +184,11 @@ sw_handle* sw_create(const sw_config* cfg) {
         size_t J = (size_t)cfg->max_total_jobs, I = (size_t)cfg->max_instances;
         if (h->d_in.reserve(in_block_bytes((int32_t)I, (int64_t)J)) ||
             h->d_res.reserve(res_block_bytes((int32_t)I, (int64_t)J, (int64_t)J * SW_MAX_ROUNDS)) ||
-            h->d_masks.reserve(J)) {
+            h->d_masks.reserve(J) || h->d_nb.reserve(J) || h->d_lvl.reserve(I) ||
+            h->d_p2ws.reserve(J * SW_P2X_ARR_BYTES) ||
+            h->h_in.reserve(in_block_bytes((int32_t)I, (int64_t)J)) ||
+            h->h_res.reserve(res_block_bytes((int32_t)I, (int64_t)J, (int64_t)J * SW_MAX_ROUNDS)) ||
+            h->h_masks.reserve(J)) {
             g_create_error = "device reservation failed";
             sw_destroy(h);
             return nullptr;

@@ -80,5 +80,5 @@ struct sw_batch_dev {
     sw_ws_dev ws;
     unsigned char* p2ws; /* P2 exchange arrays, SW_P2X_ARR_BYTES per job (sw_p2x_inst.h) */
     int32_t fuse_p2x;    /* sw_plan_kernel: run the exchange step after the solve (sw_p2x_inst.h) */
-    uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][16] cycles (8…13: pack round-loop phases) */
+    uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][SW_STAMP_SLOTS] cycles (8…13: pack round-loop phases, 16…: level search, 32…: exchange) */
 };

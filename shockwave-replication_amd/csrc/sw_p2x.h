@@ -49,6 +49,10 @@
 #define SW_P2X_KMAX 8          /* width classes handled (more: the step is skipped) */
 #define SW_P2X_NONE 1.0e300    /* "no edge" cost                                 */
 #define SW_P2X_AMAX 4096       /* active jobs handled (more: the step is skipped) */
+#define SW_P2X_ARR_BYTES 24     /* exchange workspace bytes per job: the
+                                  sw_p2x_arrays of sw_p2x_dev.h (i32 width, i32
+                                  job, f64 c, u64 mask); the host sizes the
+                                  workspace with it                             */
 #define SW_P2X_MAX_MOVES 1024  /* job moves one cycle may make (more: the cycle is
                                   not cancelled and the load size F is done)     */
 

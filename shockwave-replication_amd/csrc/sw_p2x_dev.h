@@ -35,7 +35,8 @@ struct sw_p2x_arrays {
     double* cc;   /* c = p / n                   */
     uint64_t* cm; /* round mask (improved here)  */
 };
-#define SW_P2X_ARR_BYTES 24 /* bytes per job of sw_p2x_arrays */
+static_assert(SW_P2X_ARR_BYTES == 2 * sizeof(int32_t) + sizeof(double) + sizeof(uint64_t),
+              "SW_P2X_ARR_BYTES (sw_p2x.h) must cover the sw_p2x_arrays layout");
 
 /* fixed LDS part */
 struct sw_p2x_lds {

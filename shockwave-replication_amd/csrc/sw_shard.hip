@@ -1014,18 +1014,25 @@ __global__ __launch_bounds__(256) void k_xchg(PeerSet ps, const unsigned char* s
 /* A per-process identity: 128 random bits drawn once per process, and the
  * kernel boot id (so equal nonces on two hosts cannot collide either). */
 void process_identity(unsigned long long nonce[2], char* boot, size_t boot_len) {
-    static unsigned long long n0 = 0, n1 = 0;
-    if (n0 == 0 && n1 == 0) {
+    /* drawn once per process: a function-local static is initialised exactly
+     * once even when ranks that are threads of one process call this at the
+     * same time (C++11), so every such rank sees the same nonce */
+    struct Nonce {
+        unsigned long long n0 = 0, n1 = 0;
+    };
+    static const Nonce id = [] {
+        Nonce n;
         FILE* f = fopen("/dev/urandom", "rb");
-        if (!f || fread(&n0, sizeof(n0), 1, f) != 1 || fread(&n1, sizeof(n1), 1, f) != 1) {
-            n0 = (unsigned long long)getpid() * 0x9E3779B97F4A7C15ull ^ (unsigned long long)time(nullptr);
-            n1 = (unsigned long long)(uintptr_t)&n0;
+        if (!f || fread(&n.n0, sizeof(n.n0), 1, f) != 1 || fread(&n.n1, sizeof(n.n1), 1, f) != 1) {
+            n.n0 = (unsigned long long)getpid() * 0x9E3779B97F4A7C15ull ^ (unsigned long long)time(nullptr);
+            n.n1 = (unsigned long long)(uintptr_t)&process_identity;
         }
         if (f) fclose(f);
-        if (n0 == 0 && n1 == 0) n0 = 1;
-    }
-    nonce[0] = n0;
-    nonce[1] = n1;
+        if (n.n0 == 0 && n.n1 == 0) n.n0 = 1;
+        return n;
+    }();
+    nonce[0] = id.n0;
+    nonce[1] = id.n1;
     memset(boot, 0, boot_len);
     if (FILE* b = fopen("/proc/sys/kernel/random/boot_id", "r")) {
         if (!fgets(boot, (int)boot_len, b)) boot[0] = 0;

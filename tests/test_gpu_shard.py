@@ -20,7 +20,7 @@ from test_shard import CASES, ThreadGroup, assemble, assert_same_as_single
 pytestmark = pytest.mark.gpu
 
 
-def gpu_shard_threads(a, world):
+def gpu_shard_threads(a, world, peer=False):
     group = ThreadGroup(world)
     out = [None] * world
     errs = []
@@ -29,6 +29,8 @@ def gpu_shard_threads(a, world):
         try:
             s = sn.Solver(device=0)
             s.dist_init_host(sn.HostComm(group.member(r)), r, world)
+            if peer:  # every thread enters the peer setup at once
+                s.dist_enable_peer(a.N)
             lo, hi = sn.shard_range(a.N, world, r)
             out[r] = (lo, hi, s.dist_solve(a.slice(lo, hi), lo, a.N))
             s.close()
@@ -87,6 +89,25 @@ def test_gpu_shard_c4_world8(twin):
     a = ss.synth_problem(12, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
     r = gpu_shard_threads(a, 8)
     assert_same_as_single(r, twin.solve(a), "C4 W=8")
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gpu_shard_peer_transport_threaded_ranks(world, twin):
+    """sw_dist_enable_peer with ranks that are threads of ONE process,
+    entering the setup concurrently: every rank must see the same process
+    identity (one nonce per process, initialised once) and take the
+    same-process pointer path, then one solve matches the twin.  World 2
+    only: the ranks share one GPU here, and each one's exchange kernel waits
+    on the device for the others, so their streams need hardware queues of
+    their own (GPU_MAX_HW_QUEUES = 4 per process on the box, and this module
+    already holds the RCCL handle's stream; at world 4 two ranks shared a
+    queue and the exchange timed out, include/shockwave_amd.h)."""
+    for case in (CASES[1], CASES[6]):
+        seed, N, G, T, k, lam = case
+        a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+        r = gpu_shard_threads(a, world, peer=True)
+        check_plan_valid(a, r)
+        assert_same_as_single(r, twin.solve(a), f"peer threads W={world} {case}")
 
 
 def test_gpu_shard_rejects_bad_slice(rccl_solver):

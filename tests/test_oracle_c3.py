@@ -116,6 +116,42 @@ def test_gpu_vs_oracle_headline_one_launch(gpu_solver):
 
 
 @pytest.mark.gpu
+def test_gpu_vs_oracle_benched_split_form(gpu_solver, twin):
+    """The launch form bench.py times: a batch of more than 1,024 on-chip
+    instances runs the split kernels (sw_level_kernel -> sw_pack_kernel ->
+    slow-path sw_plan_kernel -> sw_p2x_kernel, sw_api.hip split_min_count).
+    The 28 fixtures are spread through 4,096 C3 instances and the batch is
+    driven twice: device-resident (sw_batch_upload / run / download, exactly
+    the bench's timed path) and through sw_plan_solve_batch (the chunk
+    pipeline, >= 4,096 instances).  Fixtures are held to the oracle bars;
+    both forms must agree bit for bit, and a sample equals the twin."""
+    from helpers import assert_same_result
+
+    n = 4096
+    fixed = [problem(c) for c in CASES]
+    slots = [(i * 149 + 11) % n for i in range(len(CASES))]
+    assert len(set(slots)) == len(CASES)
+    batch, fi = [], 0
+    for i in range(n):
+        if i in slots:
+            batch.append(fixed[slots.index(i)])
+        else:
+            batch.append(ss.c3_problem(900_000 + i))
+    gpu_solver.upload(batch)
+    gpu_solver.run()
+    rd = gpu_solver.download()
+    rp = gpu_solver.solve_batch(batch)
+    for k, (c, s) in enumerate(zip(CASES, slots)):
+        check_against_oracle(c, batch[s], rd[s])
+        assert_same_result(rd[s], twin.solve(batch[s]), f"fixture {k} at slot {s}")
+    for i in range(n):
+        assert_same_result(rp[i], rd[i], f"pipelined vs resident, slot {i}")
+    for i in range(0, n, 64):
+        check_plan_valid(batch[i], rd[i])
+        assert_same_result(rd[i], twin.solve(batch[i]), f"slot {i}")
+
+
+@pytest.mark.gpu
 def test_gpu_c5_sweep_512_one_launch(gpu_solver, twin):
     """BASELINE config 5 at full size: 512 independent 900 x 30 instances
     (seeds x cluster sizes G in {32, 64, 128, 256}, k / lambda from the
