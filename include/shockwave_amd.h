@@ -182,8 +182,12 @@ void* sw_stream(sw_handle* h);
  * Per-kernel timing with HIP events recorded on the handle's stream around
  * each launch of sw_batch_run.  enable=1 turns it on (adds two event records
  * per kernel).  sw_kernel_times() synchronises and returns accumulated ms for
- * [0] the P2 exchange kernel (sw_p2x_kernel) and [1] the plan kernel
- * (sw_plan_kernel), plus the number of runs.
+ * [0] the P2 exchange kernel (sw_p2x_kernel) and [1] the plan kernels
+ * (sw_plan_kernel, or the split level / pack / slow-path kernels of batches
+ * above 1,024 on-chip instances), plus the number of runs.  On-chip batches
+ * of at most 256 instances (every single solve) run the exchange step fused
+ * at the end of sw_plan_kernel: there [0] reads 0 and [1] holds both, so
+ * the two stages are not separable.
  */
 int sw_set_timing(sw_handle* h, int32_t enable);
 int sw_kernel_times(sw_handle* h, double* ms_p2x, double* ms_plan, int32_t* runs);

@@ -469,6 +469,54 @@ out:
     return rc;
 }
 
+/* the per-round re-optimisation on the gathered P1 plan (twin_reround_arrays) */
+int32_t twin_reround_arrays(int32_t N, int32_t T, int32_t G, double k, int32_t nb,
+                            const double* beta, const double* ell, const sw_jobc* jc,
+                            int32_t* n, uint8_t* y, int64_t* passes);
+typedef struct {
+    sw_jobc c;
+    uint64_t m;
+    int32_t n, pad;
+} rrg_t;
+
+static int e_reround(void* ctx, int32_t* moves) {
+    eng_t* E = (eng_t*)ctx;
+    const int64_t P = E->P > 0 ? E->P : 1, N = E->N;
+    const size_t NN = N > 0 ? (size_t)N : 1;
+    rrg_t* mine = (rrg_t*)calloc((size_t)P, sizeof(rrg_t));
+    rrg_t* all = (rrg_t*)calloc((size_t)P * E->world, sizeof(rrg_t));
+    sw_jobc* jc = (sw_jobc*)malloc(sizeof(sw_jobc) * NN);
+    int32_t* n = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint8_t* y = (uint8_t*)malloc(NN * (size_t)E->T);
+    int rc = -1;
+    if (!mine || !all || !jc || !n || !y) goto out;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        mine[i].c = E->jc[i];
+        mine[i].m = E->y[SW_Y_BEST][i];
+        mine[i].n = E->arr[SW_A_NFIN][i];
+    }
+    rc = E->comm->allgather(E->comm->ctx, mine, all, P * (int64_t)sizeof(rrg_t));
+    if (rc) goto out;
+    for (int64_t j = 0; j < N; ++j) { /* blocks are P long and contiguous: job j at j */
+        jc[j] = all[j].c;
+        n[j] = all[j].n;
+        for (int32_t t = 0; t < E->T; ++t) y[(size_t)j * E->T + t] = (uint8_t)((all[j].m >> t) & 1u);
+    }
+    int64_t passes = 0;
+    *moves = twin_reround_arrays((int32_t)N, E->T, E->G, E->k, E->nb, E->beta, E->ell, jc, n, y,
+                                 &passes);
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int64_t j = E->off + i;
+        uint64_t m = 0;
+        for (int32_t t = 0; t < E->T; ++t) m |= (uint64_t)y[(size_t)j * E->T + t] << t;
+        E->y[SW_Y_BEST][i] = m;
+        E->arr[SW_A_NFIN][i] = n[j];
+    }
+out:
+    free(mine); free(all); free(jc); free(n); free(y);
+    return rc;
+}
+
 /*
  * One rank's sharded solve (same contract as sw_dist_plan_solve): `local`
  * holds this rank's jobs, [job_offset, job_offset + local->num_jobs) of
@@ -538,6 +586,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.fill_best = e_fill_best;
     ops.fill_apply = e_fill_apply;
     ops.p2x = e_p2x;
+    ops.reround = e_reround;
     ops.search = NULL; /* the controller's own K-ary loop */
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,

@@ -35,6 +35,7 @@
 #include "sw_device.h"
 #include "sw_pack.h"
 #include "sw_repair.h"
+#include "sw_reround_dev.h"
 #include "sw_p2x_inst.h"
 
 namespace {
@@ -1404,6 +1405,10 @@ __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
     if (one) {
         const size_t NJ = SW_LDS_JOBS;
         s += 8 * r16(NJ) + 3 * r16(8 * NJ) + r16(8 * 4 * SW_JPT * SW_BLOCK) + SW_JOB_LDS_BYTES;
+    } else {
+        /* the re-optimisation's knapsack rows and take bits (sw_reround_dev.h;
+         * on chip they reuse the sort buffer and two mask rows) */
+        s += 2 * r16(8 * (SW_RR_CAPMAX + 1)) + r16(8 * SW_RR_WORDS);
     }
     return s;
 }
@@ -1689,6 +1694,43 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
 }
 
+/* The re-optimisation's view of an instance (sw_reround_dev.h): the best P1
+ * plan ybest / nfin; on chip the per-job values in registers, otherwise in
+ * workspace rows that are free between P1 and P2. */
+template <int KT, bool ONE>
+struct RREnv {
+    Ctx<KT, ONE>& c;
+    sw_blk& blk;
+    int N, T, G;
+    double k;
+    uint8_t *S, *Sb;
+    uint32_t* items;
+    double *iv, *dpA, *dpB;
+    uint64_t* bits;
+    double rv[SW_JPT], r0[SW_JPT], r1[SW_JPT]; /* ONE */
+    double *gv, *g0, *g1;                      /* !ONE */
+    __device__ RREnv(Ctx<KT, ONE>& cc) : c(cc), blk(cc.blk) {}
+    template <class F>
+    __device__ __forceinline__ void for_jobs(F&& f) { c.for_jobs(f); }
+    __device__ __forceinline__ sw_jobc jc(int j) const { return c.jc(j, 0); }
+    __device__ __forceinline__ double f(const sw_jobc& q, int n) const {
+        return sw_f(&q, n, c.nb, c.beta, c.ell, c.slope);
+    }
+    __device__ __forceinline__ bool tj(int j) const { return c.jc(j, 0).w <= G; }
+    __device__ __forceinline__ uint64_t& y(int j) { return c.ybest[j]; }
+    __device__ __forceinline__ int cnt(int j) const { return c.nfin[j]; }
+    __device__ __forceinline__ void add_cnt(int j, int d) { c.nfin[j] = (uint8_t)(c.nfin[j] + d); }
+    __device__ __forceinline__ double& V(int j, int s) {
+        if constexpr (ONE) { (void)j; return rv[s]; } else { (void)s; return gv[j]; }
+    }
+    __device__ __forceinline__ double& H0(int j, int s) {
+        if constexpr (ONE) { (void)j; return r0[s]; } else { (void)s; return g0[j]; }
+    }
+    __device__ __forceinline__ double& H1(int j, int s) {
+        if constexpr (ONE) { (void)j; return r1[s]; } else { (void)s; return g1[j]; }
+    }
+};
+
 template <int KT, bool ONE>
 __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned char* smem,
                                                          int inst_) {
@@ -1738,6 +1780,8 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
     c.pwc = 0;
     c.misc = (int64_t*)carve(sizeof(int64_t) * 8);
     c.rep = (sw_repair_t*)carve(sizeof(sw_repair_t));
+    double *rr_dpA = nullptr, *rr_dpB = nullptr; /* !ONE: LDS for the re-optimisation */
+    uint64_t* rr_bits = nullptr;
     if (threadIdx.x < SW_BMAX) {
         const int b = (int)threadIdx.x;
         bt[b] = I->beta[b];
@@ -1795,6 +1839,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.sbuf = B.ws.sort + 4 * jo;
         c.gkeys = B.ws.keys + (size_t)KT * jo;
         c.gjc = B.ws.jc + jo;
+        rr_dpA = (double*)carve(8 * (SW_RR_CAPMAX + 1));
+        rr_dpB = (double*)carve(8 * (SW_RR_CAPMAX + 1));
+        rr_bits = (uint64_t*)carve(8 * SW_RR_WORDS);
         for (int j = c.jlo(); j < c.jhi(); ++j)
             c.gjc[j] = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
                                     B.E[jo + j], B.R[jo + j], B.p[jo + j]);
@@ -1945,6 +1992,40 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             __syncthreads();
         }
         if (added > 0) {
+            dens_best = false;
+            rep_best = false;
+            dskip_best = false;
+        }
+        /* ... and re-optimise it round by round (twin: twin_reround_arrays).
+         * Its scratch is the P1 level-search / packing state, dead here; on
+         * chip: items in the level-search bytes, values in registers, the
+         * knapsack rows in ycur / y2, take bits and item values in the sort
+         * buffer */
+        RREnv<KT, ONE> e(c);
+        e.N = c.N;
+        e.T = c.T;
+        e.G = c.G;
+        e.k = c.k;
+        e.S = c.placed;
+        e.Sb = c.placed2;
+        if constexpr (ONE) {
+            e.items = reinterpret_cast<uint32_t*>(c.ncur);
+            e.bits = c.sbuf;
+            e.iv = reinterpret_cast<double*>(c.sbuf + SW_RR_WORDS);
+            e.dpA = reinterpret_cast<double*>(c.ycur);
+            e.dpB = reinterpret_cast<double*>(c.y2);
+            e.gv = e.g0 = e.g1 = nullptr;
+        } else {
+            e.items = c.pst;
+            e.iv = reinterpret_cast<double*>(c.pord);
+            e.gv = reinterpret_cast<double*>(c.ycur);
+            e.g0 = reinterpret_cast<double*>(c.y2);
+            e.g1 = reinterpret_cast<double*>(c.pmask);
+            e.dpA = rr_dpA;
+            e.dpB = rr_dpB;
+            e.bits = rr_bits;
+        }
+        if (sw_rr_run(e, c.passes) > 0) {
             dens_best = false;
             rep_best = false;
             dskip_best = false;

@@ -62,6 +62,7 @@
 #include "sw_p2x.h"
 #include "sw_p2x_dev.h"
 #include "sw_pack.h"
+#include "sw_reround_dev.h"
 #include "sw_shard_ctl.h"
 #include "sw_validate.h"
 
@@ -888,6 +889,118 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all
     if (threadIdx.x == 0) S.red[0] = nc;
 }
 
+/* ---- per-round re-optimisation (sw_reround_dev.h) on the gathered P1 plan ----
+ * Two 24-byte gathers per job (the pack's entry size, so the peer regions
+ * hold them): the inputs (d, R, p) and (mask, count, w, F, E); every rank
+ * rebuilds every job's constants with sw_make_jobc — the same bits its owner
+ * computed — and runs the step on one workgroup, then keeps its own rows. */
+struct rr_in {
+    double d, R, p;
+};
+struct rr_row {
+    uint64_t m;
+    int32_t n, w, F, E;
+};
+static_assert(sizeof(rr_in) == sizeof(sw_pack_ent) && sizeof(rr_row) == sizeof(sw_pack_ent),
+              "re-optimisation entries use the pack's gather size");
+
+__global__ __launch_bounds__(kTB) void k_rr_ent(ShardDev S, const int32_t* w, const int32_t* F,
+                                                const int32_t* E, const double* d, const double* R,
+                                                const double* pr, rr_in* in, rr_row* row) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i >= S.P) return;
+    rr_in a;
+    rr_row b;
+    a.d = a.R = a.p = 0.0;
+    b.m = 0; b.n = 0; b.w = 1; b.F = 0; b.E = 1;
+    if (i < S.NL) {
+        a.d = d[i]; a.R = R[i]; a.p = pr[i];
+        b.m = S.y[SW_Y_BEST][i]; b.n = S.arr[SW_A_NFIN][i]; b.w = w[i]; b.F = F[i]; b.E = E[i];
+    }
+    in[i] = a;
+    row[i] = b;
+}
+
+/* The step's view of the gathered instance: per-job values in the workspace
+ * (JMAX = 0 form of sw_reround_dev.h). */
+struct ShardRREnv {
+    sw_blk& blk;
+    int N, T, G, q, nb;
+    double k;
+    const double *beta, *ell, *slope;
+    const sw_jobc* jcg;
+    uint64_t* yg;
+    int32_t* ng;
+    double *gv, *g0, *g1;
+    uint8_t *S, *Sb;
+    uint32_t* items;
+    double *iv, *dpA, *dpB;
+    uint64_t* bits;
+    __device__ ShardRREnv(sw_blk& b) : blk(b) {}
+    template <class F>
+    __device__ __forceinline__ void for_jobs(F&& f) {
+        const int j0 = (int)threadIdx.x * q, j1 = j0 + q < N ? j0 + q : N;
+        for (int j = j0; j < j1; ++j) f(j, 0);
+    }
+    __device__ __forceinline__ sw_jobc jc(int j) const { return jcg[j]; }
+    __device__ __forceinline__ double f(const sw_jobc& c, int n) const {
+        return sw_f(&c, n, nb, beta, ell, slope);
+    }
+    __device__ __forceinline__ bool tj(int j) const { return jcg[j].w <= G; }
+    __device__ __forceinline__ uint64_t& y(int j) { return yg[j]; }
+    __device__ __forceinline__ int cnt(int j) const { return ng[j]; }
+    __device__ __forceinline__ void add_cnt(int j, int d) { ng[j] += d; }
+    __device__ __forceinline__ double& V(int j, int) { return gv[j]; }
+    __device__ __forceinline__ double& H0(int j, int) { return g0[j]; }
+    __device__ __forceinline__ double& H1(int j, int) { return g1[j]; }
+};
+
+__global__ __launch_bounds__(SW_BLOCK) void k_rr(ShardDev S, double delta, const rr_in* in,
+                                                 const rr_row* row, unsigned char* ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int N = (int)S.N;
+    sw_blk blk;
+    blk.X = reinterpret_cast<sw_xchg*>(smem);
+    blk.par = 0;
+    size_t off = (sizeof(sw_xchg) + 15) & ~(size_t)15;
+    ShardRREnv e(blk);
+    e.dpA = reinterpret_cast<double*>(smem + off);
+    e.dpB = e.dpA + (SW_RR_CAPMAX + 1);
+    e.bits = reinterpret_cast<uint64_t*>(e.dpB + (SW_RR_CAPMAX + 1));
+    const size_t M = (size_t)(N > 0 ? N : 1);
+    sw_jobc* jcg = reinterpret_cast<sw_jobc*>(ws);
+    unsigned char* p = ws + ((M * sizeof(sw_jobc) + 15) & ~(size_t)15);
+    e.yg = reinterpret_cast<uint64_t*>(p); p += 8 * M;
+    e.gv = reinterpret_cast<double*>(p); p += 8 * M;
+    e.g0 = reinterpret_cast<double*>(p); p += 8 * M;
+    e.g1 = reinterpret_cast<double*>(p); p += 8 * M;
+    e.iv = reinterpret_cast<double*>(p); p += 8 * SW_RR_WORDS;
+    e.ng = reinterpret_cast<int32_t*>(p); p += 4 * M;
+    e.items = reinterpret_cast<uint32_t*>(p); p += 4 * SW_RR_WORDS;
+    e.S = p; p += M;
+    e.Sb = p;
+    e.jcg = jcg;
+    e.N = N; e.T = S.T; e.G = S.G; e.k = S.k; e.nb = S.nb;
+    e.q = (N + SW_BLOCK - 1) / SW_BLOCK;
+    e.beta = S.beta; e.ell = S.ell; e.slope = S.slope;
+    for (int j = threadIdx.x; j < N; j += SW_BLOCK) {
+        const rr_in a = in[j];
+        const rr_row b = row[j];
+        jcg[j] = sw_make_jobc(N, S.T, delta, b.w, a.d, b.F, b.E, a.R, a.p);
+        e.yg[j] = b.m;
+        e.ng[j] = b.n;
+    }
+    __syncthreads();
+    int64_t passes = 0;
+    const int moves = sw_rr_run(e, passes);
+    if (moves > 0)
+        for (int i = threadIdx.x; i < S.NL; i += SW_BLOCK) {
+            S.y[SW_Y_BEST][i] = e.yg[S.off + i];
+            S.arr[SW_A_NFIN][i] = e.ng[S.off + i];
+        }
+    if (threadIdx.x == 0) S.red[0] = moves;
+}
+
 /* Step results to the host without a stream synchronisation: the words are
  * stored into fine-grained pinned host memory, then a sequence number is
  * released at system scope; the host spins on it (sw_shard_state::publish).
@@ -1089,6 +1202,7 @@ struct sw_shard_state {
     DevBuf<long long> red, tieblk;
     DevBuf<sw_pack_ent> pall;
     DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry) */
+    DevBuf<unsigned char> rrin, rrrow, rrws; /* re-optimisation: gathered entries, workspace */
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
@@ -1646,6 +1760,38 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
     return SW_OK;
 }
 
+/* twin: e_reround (oracle/shard_twin.c) — gather the P1 plan and every job's
+ * inputs, run the re-optimisation replicated, keep this rank's rows */
+int op_reround(void* ctx, int32_t* moves) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    const int64_t M = S->P * S->world;
+    const size_t Mj = (size_t)std::max<int64_t>(S->N, 1);
+    const size_t wsb = ((Mj * sizeof(sw_jobc) + 15) & ~(size_t)15) + 8 * Mj * 4 + 8 * SW_RR_WORDS +
+                       4 * Mj + 4 * SW_RR_WORDS + 2 * Mj + 16;
+    if (S->rrin.reserve((size_t)M * sizeof(rr_in)) || S->rrrow.reserve((size_t)M * sizeof(rr_row)) ||
+        S->rrws.reserve(wsb))
+        return host_fail(S, "re-optimisation workspace");
+    rr_in* in_all = reinterpret_cast<rr_in*>(S->rrin.p);
+    rr_row* row_all = reinterpret_cast<rr_row*>(S->rrrow.p);
+    rr_in* in_mine = in_all + (size_t)S->rank * S->P;
+    rr_row* row_mine = row_all + (size_t)S->rank * S->P;
+    LAUNCH(S, k_rr_ent, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, S->in_w, S->in_F, S->in_E,
+           S->in_d, S->in_R, S->in_p, in_mine, row_mine);
+    /* in place: each rank's block is already where the gather puts it */
+    SH_TRY(coll_gather(S, in_mine, in_all, (size_t)S->P * sizeof(rr_in), nullptr));
+    SH_TRY(coll_gather(S, row_mine, row_all, (size_t)S->P * sizeof(rr_row), nullptr));
+    SH_TRY(zero_red(S, 1));
+    const size_t lds = ((sizeof(sw_xchg) + 15) & ~(size_t)15) + 2 * 8 * (SW_RR_CAPMAX + 1) +
+                       8 * SW_RR_WORDS;
+    LAUNCH(S, k_rr, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, S->delta, (const rr_in*)in_all,
+           (const rr_row*)row_all, S->rrws.p);
+    uint64_t mv = 0;
+    SH_TRY(coll_reduce(S, S->dv.red, 1, 1, &mv)); /* every rank computed the same count */
+    *moves = (int32_t)mv;
+    return SW_OK;
+}
+
 /* Reserve the per-solve buffers and upload this rank's jobs. */
 int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, bool dev,
             const sw_result* res) {
@@ -1749,7 +1895,7 @@ void sw_shard_release(sw_handle* h) {
     S->tie.release(); S->tieblk.release(); S->xa.release();
     S->planned.release(); S->porder.release(); S->d.release(); S->R.release();
     S->p.release(); S->xrecv.release(); S->jc.release(); S->keys.release();
-    S->plan.release(); S->red.release(); S->pall.release(); S->p2ws.release(); S->hx.release();
+    S->plan.release(); S->red.release(); S->pall.release(); S->p2ws.release(); S->rrin.release(); S->rrrow.release(); S->rrws.release(); S->hx.release();
     if (S->pub) (void)hipHostFree(S->pub);
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
@@ -2008,6 +2154,7 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.class_caps = op_class_caps;
     ops.pack_class = op_pack_class;
     ops.p2x = op_p2x;
+    ops.reround = op_reround;
     ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,

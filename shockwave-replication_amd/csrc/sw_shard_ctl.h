@@ -128,6 +128,11 @@ typedef struct sw_shard_ops {
      * arr[nsrc]: the active jobs' rows are gathered, the step runs on every
      * rank alike and each rank keeps its own rows; *cancels = cycles applied */
     int (*p2x)(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels);
+    /* per-round exact re-optimisation (sw_reround.h) of the re-solved P1
+     * plan Y[SW_Y_BEST] / arr[SW_A_NFIN]: every job's constants, row and
+     * count are gathered, the step runs on every rank alike and each rank
+     * keeps its own rows and counts; *moves = rounds whose set changed */
+    int (*reround)(void* ctx, int32_t* moves);
     /* optional (NULL = the controller drives count_gt / feasible itself):
      * the whole K-ary search of swc_search inside the engine — kind 0 over
      * count_gt, 1 over feasible — returning its answer and the number of
@@ -531,6 +536,15 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                 ++added;
             }
             if (added > 0) {
+                dens_best = 0;
+                rep_best = 0;
+                dskip_best = 0;
+            }
+            /* ... and re-optimise it round by round (twin_reround_arrays) */
+            int32_t moves = 0;
+            SWC_RUN(o->reround(o->ctx, &moves));
+            c->steps++;
+            if (moves > 0) {
                 dens_best = 0;
                 rep_best = 0;
                 dskip_best = 0;
