@@ -128,6 +128,7 @@ def parse():
 
 CPU_SEEDS = (0, 1, 2)  # fixed C3 seeds of the CPU leg (sw_synth seeds 10000+)
 CPU_LIMIT_S = 15.0  # the reference's per-MILP TimeLimit (scale_*gpus.json, shockwave.py:405)
+ALL_CORES = 16  # host cores per GPU on the MI355X box (OMP_NUM_THREADS there)
 
 
 def _cpu_model():
@@ -171,6 +172,23 @@ def cpu_baseline(args):
             p.kill()
             outs.append({"seconds": None, "status": f"failed: {e!r}"})
     solves, relax = outs[:-1], outs[-1]
+    # (ii) all cores: one single-threaded process per core of this GPU's host
+    # share, each on its own C3 instance (C5-style replicas), after the
+    # latency leg so the two never share cores
+    ncores = max(1, min(ALL_CORES, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    many = [subprocess.Popen([sys.executable, tool, "--one", str(100 + i)], stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, env=env, text=True) for i in range(ncores)]
+    mouts = []
+    for p in many:
+        try:
+            o, _ = p.communicate(timeout=4 * CPU_LIMIT_S + 60)
+            mouts.append(json.loads(o.strip().splitlines()[-1]))
+        except Exception as e:
+            p.kill()
+            mouts.append({"seconds": None, "status": f"failed: {e!r}"})
+    wall = time.perf_counter() - t0
+    done = sum(1 for o in mouts if o.get("seconds") is not None and o.get("status") != "no_solution")
     secs = sorted(o["seconds"] for o in solves if o.get("seconds") is not None)
     med = secs[len(secs) // 2] if secs else None
     labels = [f"seed {s}: {o.get('seconds') or float('nan'):.2f} s, P1 {o.get('status')}"
@@ -191,6 +209,13 @@ def cpu_baseline(args):
         "no_incumbent_seeds": [s for s, o in zip(CPU_SEEDS, solves) if o.get("status") == "no_solution"],
         "lp_only_s": relax.get("seconds"),
         "lp_only_note": "LP relaxation of P1 alone (x, SOS2 binaries continuous; no rounding, no P2), seed 0",
+        "all_cores": {"processes": ncores, "instances": ncores, "wall_s": wall, "completed": done,
+                      "plan_solves_per_s": done / wall if wall > 0 else None,
+                      "attempted_per_s": ncores / wall if wall > 0 else None,
+                      "note": "one single-threaded HiGHS process per core, each its own C3 seed "
+                              "(sw_synth 10100+), started together; completed = a P1 incumbent "
+                              "within the 15 s limit (the others are the reference's "
+                              "AssertionError)"},
         "host": {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
                  "cpu_model": _cpu_model()},
     }
