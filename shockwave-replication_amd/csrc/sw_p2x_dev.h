@@ -5,17 +5,18 @@
  * sharded engine on its gathered placement (sw_shard.hip).
  *
  * Mapping.  Active jobs are ranked inside their width class by (c desc, job
- * asc) with an all-pairs count (LDS tiles), and each class's membership of
- * each round becomes a rank bitset in LDS, so the move an edge t → u makes is
- * a few 64-bit and-not / ctz / clz word operations.  Edge costs W[t][u] are
- * built by all threads, one (t, u) pair per thread, once per load size F and
- * afterwards only in the rows and columns of the rounds a cancelled cycle
- * touched (the other entries cannot change).  Wave 0 runs Bellman–Ford with
- * one round per lane: the relaxations read the other lanes' distances with
- * readlane (the round index is wave-uniform), the free-capacity node V is a
- * wave-uniform scalar, and the predecessor check uses pointer doubling
- * (7 shuffles reach 128 ≥ T + 1 steps).  A cycle's moves are applied with LDS
- * atomics.
+ * asc) with a bitonic sort (shuffles below stride 64, LDS above), and each
+ * class's membership of each round becomes a rank bitset in LDS (one wave
+ * ballot per 64-rank word), so the move an edge t → u makes is a few 64-bit
+ * and-not / ctz / clz word operations.  Edge costs W[t][u] are built by all
+ * threads, one (t, u) pair per thread, once per load size F and afterwards
+ * only in the rows and columns of the rounds a cancelled cycle touched (the
+ * other entries cannot change).  Bellman–Ford is block-wide: waves 0–3 relax
+ * a quarter of the source rounds each (lane = target round), wave 0 combines
+ * them, handles the free-capacity node V as a wave-uniform scalar and checks
+ * the predecessor graph by pointer doubling (7 shuffles reach 128 ≥ T + 1
+ * steps); each load size's runs start from its previous run's distances.  A
+ * cycle's moves are applied with LDS atomics.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -58,6 +59,7 @@ struct sw_p2x_lds {
     int32_t pt[4][64];
     int32_t bfdone;
     int32_t fq[SW_P2X_KMAX]; /* F / w_k for the current load size (0: w_k ∤ F) */
+    double dw[SW_P2X_KMAX][SW_TMAX + 1]; /* each load size's last Bellman–Ford distances */
 };
 
 /* LDS the variable part needs for up to maxA active jobs and T rounds:
@@ -90,7 +92,7 @@ static __device__ __forceinline__ int p2x_class(const sw_p2x_lds* L, int32_t w) 
  * (7 shuffles reach 128 ≥ T + 1 steps).  Leaves the cycle in L->cyc / L->len
  * (0: none).  All threads call it. */
 static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const double* W, int T, int F,
-                                                      uint64_t* sp = nullptr) {
+                                                      double* dw, bool warm, uint64_t* sp = nullptr) {
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     (void)sp;
 #ifdef SW_STAMPS
@@ -109,8 +111,8 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
     } while (0)
 #endif
     const bool act = lane < T;
-    if (tid <= T) {
-        L->bd[tid] = 0.0;
+    if (tid <= T) { /* from this load size's last distances when warm (twin: find_cycle) */
+        L->bd[tid] = warm ? dw[tid] : 0.0;
         L->bp[tid] = -1;
     }
     if (tid == 0) L->bfdone = 0;
@@ -232,6 +234,7 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
         __syncthreads();
         if (L->bfdone) break;
     }
+    if (tid <= T) dw[tid] = L->bd[tid]; /* read by this thread's next init only */
 #undef BF_STAMP
 }
 
@@ -650,6 +653,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     int cert[SW_P2X_KMAX];
 #pragma unroll
     for (int k = 0; k < SW_P2X_KMAX; ++k) cert[k] = -1;
+    uint32_t havem = 0; /* load sizes with distances in L->dw (warm starts) */
     for (bool changed = true; changed && ncancel < SW_P2X_MAX_CANCEL;) {
         changed = false;
         for (int ki = 0; ki < K && ncancel < SW_P2X_MAX_CANCEL; ++ki) {
@@ -671,7 +675,8 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
 #ifdef SW_STAMPS
                 if (threadIdx.x == 0 && sp) sp[8] += 1;
 #endif
-                p2x_find_cycle(L, W, T, F, sp);
+                p2x_find_cycle(L, W, T, F, L->dw[ki], ((havem >> ki) & 1u) != 0, sp);
+                havem |= 1u << ki;
                 P2X_STAMP(4);
                 const int len = L->len;
                 if (len == 0) {
