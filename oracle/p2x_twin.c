@@ -60,7 +60,7 @@ static void build_w(p2x_t* X, int32_t F, double delta) {
             if (u != t) {
                 for (int32_t k = 0; k < X->K; ++k) {
                     if (X->wc[k] > F || F % X->wc[k] != 0 || F / X->wc[k] > SW_P2X_QMAX) continue;
-                    const double cost = sw_p2x_cost(bits(X, k, t), bits(X, k, u), X->nw[k], F / X->wc[k],
+                    const double cost = sw_p2x_cost(bits(X, k, t), bits(X, k, u), X->nw[k], 1, F / X->wc[k],
                                                     t, u, X->pc + X->off[k]);
                     if (cost < best) { best = cost; bk = k; }
                 }
@@ -157,11 +157,11 @@ static void cancel(p2x_t* X, int32_t F, const int32_t* cyc, int32_t len, int32_t
         if (u == T || t == T) continue;
         const int32_t k = X->Wk[t * T + u];
         const int32_t q = F / X->wc[k];
-        int32_t r = sw_p2x_start(bits(X, k, t), bits(X, k, u), X->nw[k], q, u < t);
+        int32_t r = sw_p2x_start(bits(X, k, t), bits(X, k, u), X->nw[k], 1, q, u < t);
         for (int32_t g = 0; g < q; ++g) {
             tmp[nsel++] = (k << 24) | (t << 16) | (u << 8);
             tmp[nsel++] = r;
-            if (g + 1 < q) r = sw_p2x_next(bits(X, k, t), bits(X, k, u), X->nw[k], r + 1);
+            if (g + 1 < q) r = sw_p2x_next(bits(X, k, t), bits(X, k, u), X->nw[k], 1, r + 1);
         }
     }
     for (int32_t i = 0; i < nsel; i += 2) {
@@ -253,15 +253,25 @@ int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const 
     int32_t ncancel = 0;
     double dw[SW_P2X_KMAX][SW_TMAX + 1]; /* each load size's last distances */
     int have[SW_P2X_KMAX] = {0};
+    /* cert[k]: the cancel count when load size k last found no cycle; while
+     * nothing was cancelled since, its graph is unchanged and the repeat pass
+     * skips it (a warm rerun could continue a descent the last run stopped
+     * at its sweep limit, so the skip is part of the specification) */
+    int32_t cert[SW_P2X_KMAX];
+    for (int32_t k = 0; k < SW_P2X_KMAX; ++k) cert[k] = -1;
     for (int changed = 1; changed && ncancel < SW_P2X_MAX_CANCEL;) {
         changed = 0;
         for (int32_t ki = 0; ki < X->K && ncancel < SW_P2X_MAX_CANCEL; ++ki) {
             const int32_t F = X->wc[ki];
+            if (cert[ki] == ncancel) continue;
             while (ncancel < SW_P2X_MAX_CANCEL) {
                 build_w(X, F, delta);
                 const int32_t len = find_cycle(X, F, cyc, dw[ki], have[ki]);
                 have[ki] = 1;
-                if (len == 0) break;
+                if (len == 0) {
+                    cert[ki] = ncancel;
+                    break;
+                }
                 int32_t moves = 0; /* the cycle's job moves */
                 for (int32_t i = 0; i < len; ++i) {
                     const int32_t u = cyc[i], t = cyc[(i + 1) % len];

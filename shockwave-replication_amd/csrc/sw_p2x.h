@@ -74,29 +74,31 @@ SW_HD double sw_p2x_delta(double P0, int32_t T, int32_t A) {
 SW_HD uint64_t sw_p2x_ckey(double c) { return sw_bits(c) >> 3; }
 
 /* The ranks the edge t → u moves in one class: X = Bt & ~Bu over the class's
- * rank bitset (nw words; rank r = bit r % 64 of word r / 64, ranks in
+ * rank bitset (nw words, word i at B[i·ws]: the GPU stores a class's words
+ * word-major, ws = T, so the lanes of a wave reading one word of T rounds hit
+ * consecutive addresses; the twin round-major, ws = 1; rank r = bit r % 64 of word r / 64, ranks in
  * (c desc, job asc) order) — the q lowest ranks of X when lo (u < t: the
  * largest c), else its q highest.  sw_p2x_start returns the lowest selected
  * rank (-1 when X has fewer than q ranks: no edge for this class);
  * sw_p2x_next(r) the smallest rank ≥ r of X, so the selection is start,
  * next(start + 1), ... (q ranks, ascending). */
-SW_HD int32_t sw_p2x_start(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t q,
-                           int32_t lo) {
+SW_HD int32_t sw_p2x_start(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t ws,
+                           int32_t q, int32_t lo) {
     int32_t acc = 0;
     if (lo) {
         for (int32_t i = 0; i < nw; ++i) {
-            const uint64_t x = Bt[i] & ~Bu[i];
+            const uint64_t x = Bt[i * ws] & ~Bu[i * ws];
             if (x) {
                 int32_t tot = acc;
                 for (int32_t k = i; k < nw && tot < q; ++k)
-                    tot += __builtin_popcountll(Bt[k] & ~Bu[k]);
+                    tot += __builtin_popcountll(Bt[k * ws] & ~Bu[k * ws]);
                 return tot >= q ? 64 * i + __builtin_ctzll(x) : -1;
             }
         }
         return -1;
     }
     for (int32_t i = nw - 1; i >= 0; --i) {
-        uint64_t x = Bt[i] & ~Bu[i];
+        uint64_t x = Bt[i * ws] & ~Bu[i * ws];
         const int32_t cnt = __builtin_popcountll(x);
         if (acc + cnt >= q) {
             /* keep the (q − acc) highest bits of x: drop its lowest ones */
@@ -108,13 +110,13 @@ SW_HD int32_t sw_p2x_start(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, i
     return -1;
 }
 
-SW_HD int32_t sw_p2x_next(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t r) {
+SW_HD int32_t sw_p2x_next(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t ws, int32_t r) {
     int32_t i = r >> 6;
     if (i >= nw) return -1;
-    uint64_t x = (Bt[i] & ~Bu[i]) & (~0ull << (r & 63));
+    uint64_t x = (Bt[i * ws] & ~Bu[i * ws]) & (~0ull << (r & 63));
     while (!x) {
         if (++i >= nw) return -1;
-        x = Bt[i] & ~Bu[i];
+        x = Bt[i * ws] & ~Bu[i * ws];
     }
     return 64 * i + __builtin_ctzll(x);
 }
@@ -123,13 +125,13 @@ SW_HD int32_t sw_p2x_next(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, in
  * selection order (ascending ranks when u < t, descending when u > t),
  * times (u − t); SW_P2X_NONE when X has fewer than q ranks.  c is the
  * class's c array indexed by rank.  One pass over the words. */
-SW_HD double sw_p2x_cost(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t q, int32_t t,
-                         int32_t u, const double* c) {
+SW_HD double sw_p2x_cost(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int32_t ws, int32_t q,
+                         int32_t t, int32_t u, const double* c) {
     double s = 0.0;
     int32_t got = 0;
     if (u < t) {
         for (int32_t i = 0; i < nw && got < q; ++i) {
-            uint64_t x = Bt[i] & ~Bu[i];
+            uint64_t x = Bt[i * ws] & ~Bu[i * ws];
             while (x && got < q) {
                 s = s + c[64 * i + __builtin_ctzll(x)];
                 x &= x - 1;
@@ -138,7 +140,7 @@ SW_HD double sw_p2x_cost(const uint64_t* Bt, const uint64_t* Bu, int32_t nw, int
         }
     } else {
         for (int32_t i = nw - 1; i >= 0 && got < q; --i) {
-            uint64_t x = Bt[i] & ~Bu[i];
+            uint64_t x = Bt[i * ws] & ~Bu[i * ws];
             while (x && got < q) {
                 const int32_t b = 63 - __builtin_clzll(x);
                 s = s + c[64 * i + b];

@@ -193,9 +193,10 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
                     L->bd[T] = m;
                     L->bp[T] = prV;
                 }
-                /* after the odd sweeps and the last (after the first, every
-                 * predecessor is a later round: no cycle can exist yet) */
-                if ((it & 1) || it == T) {
+                /* after the odd sweeps and the last (from d = 0, after the
+                 * first every predecessor is a later round: no cycle can
+                 * exist yet; from warm distances also after the first) */
+                if ((it & 1) || it == T || (warm && it == 0)) {
                     int y = act ? pr : -1, yV = prV;
                     for (int s2 = 0; s2 < 7; ++s2) {
                         const int g = __shfl(y, (y >= 0 && y < T) ? y : 0, 64);
@@ -244,13 +245,13 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
  * takes the first set bit (lowest, or highest when descending) of the first
  * non-empty word with selects only; the c loads are then issued together and
  * summed in selection order (the same sum).  Other cases: sw_p2x_cost. */
-static __device__ __forceinline__ double p2x_cost_dev(const uint64_t* Bt, const uint64_t* Bu, int nw, int q,
-                                                      int t, int u, const double* c) {
-    if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, q, t, u, c);
+static __device__ __forceinline__ double p2x_cost_dev(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
+                                                      int q, int t, int u, const double* c) {
+    if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, ws, q, t, u, c);
     const bool lo = u < t;
     uint64_t x[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = i < nw ? (Bt[i] & ~Bu[i]) : 0ull;
+    for (int i = 0; i < 4; ++i) x[i] = i < nw ? (Bt[i * ws] & ~Bu[i * ws]) : 0ull;
     /* y[s] = the s-th word in scan order */
     uint64_t y[4];
 #pragma unroll
@@ -302,8 +303,8 @@ static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const ui
                 const int q = L->fq[k];
                 if (q == 0) continue;
                 const int nw = L->nw[k];
-                const uint64_t* Bk = B + L->boff[k];
-                const double cost = p2x_cost_dev(Bk + t * nw, Bk + u * nw, nw, q, t, u, pc + L->off[k]);
+                const uint64_t* Bk = B + L->boff[k]; /* word-major: word w of round t at w·T + t */
+                const double cost = p2x_cost_dev(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k]);
                 if (cost < best) {
                     best = cost;
                     bk = k;
@@ -610,19 +611,19 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             while (w >= L->nw[k]) w -= L->nw[k++];
             const int r = 64 * w + lane;
             const uint64_t m = r < L->M[k] ? X.cm[ord[L->off[k] + r]] : 0ull;
-            uint64_t* Bk = B + L->boff[k] + w;
+            uint64_t* Bk = B + L->boff[k] + (size_t)w * T;
             for (int t = 0; t < T; ++t) {
                 const uint64_t word = __ballot((m >> t) & 1ull);
-                if (lane == 0) Bk[t * L->nw[k]] = word;
+                if (lane == 0) Bk[t] = word;
             }
         }
         __syncthreads();
         if (tid < T) { /* G minus the round's width: Σ_k w_k · members of class k in t */
             int32_t used = 0;
             for (int k = 0; k < K; ++k) {
-                const uint64_t* Bk = B + L->boff[k] + tid * L->nw[k];
+                const uint64_t* Bk = B + L->boff[k] + tid;
                 int32_t c = 0;
-                for (int w = 0; w < L->nw[k]; ++w) c += __popcll(Bk[w]);
+                for (int w = 0; w < L->nw[k]; ++w) c += __popcll(Bk[w * T]);
                 used += c * L->wc[k];
             }
             L->room[tid] = G - used;
@@ -707,13 +708,13 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                         const int incl = wave_incscan_i32(q);
                         if (real) tm |= (1ull << t) | (1ull << u);
                         if (real && moves <= SW_P2X_MAX_MOVES) {
-                            const uint64_t* Bt = B + L->boff[k] + t * L->nw[k];
-                            const uint64_t* Bu = B + L->boff[k] + u * L->nw[k];
-                            int r = sw_p2x_start(Bt, Bu, L->nw[k], q, u < t);
+                            const uint64_t* Bt = B + L->boff[k] + t;
+                            const uint64_t* Bu = B + L->boff[k] + u;
+                            int r = sw_p2x_start(Bt, Bu, L->nw[k], T, q, u < t);
                             int n = n0 + incl - q;
                             for (int g = 0; g < q; ++g) {
                                 rec[n++] = (k << 29) | (t << 23) | (u << 17) | r;
-                                if (g + 1 < q) r = sw_p2x_next(Bt, Bu, L->nw[k], r + 1);
+                                if (g + 1 < q) r = sw_p2x_next(Bt, Bu, L->nw[k], T, r + 1);
                             }
                         }
                         n0 += __shfl(incl, 63, 64);
@@ -737,8 +738,8 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                     const int k = (v >> 29) & 7, t = (v >> 23) & 63, u = (v >> 17) & 63, r = v & 0x1FFFF;
                     uint64_t* Bk = B + L->boff[k];
                     const uint64_t bit = 1ull << (r & 63);
-                    atomicAnd((unsigned long long*)&Bk[t * L->nw[k] + (r >> 6)], ~bit);
-                    atomicOr((unsigned long long*)&Bk[u * L->nw[k] + (r >> 6)], bit);
+                    atomicAnd((unsigned long long*)&Bk[(r >> 6) * T + t], ~bit);
+                    atomicOr((unsigned long long*)&Bk[(r >> 6) * T + u], bit);
                     atomicXor((unsigned long long*)&X.cm[ord[L->off[k] + r]], (1ull << t) | (1ull << u));
                     atomicAdd(&L->room[t], L->wc[k]);
                     atomicAdd(&L->room[u], -L->wc[k]);

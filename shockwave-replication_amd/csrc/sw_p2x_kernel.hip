@@ -45,3 +45,4 @@ extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, h
     hipLaunchKernelGGL(sw_p2x_kernel, grid, block, lds, stream, *B);
     return hipGetLastError();
 }
+

@@ -29,7 +29,7 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU oracle runs")
 
 
-TWIN_SO = os.path.join(ORACLE, "_build", "libplan_twin.so")
+TWIN_SO = os.environ.get("SW_TWIN_PATH") or os.path.join(ORACLE, "_build", "libplan_twin.so")
 
 
 def _build_twin():
