@@ -118,6 +118,10 @@ struct sw_job_lds {
 
 /* jobs per thread on the on-chip path (N ≤ SW_LDS_JOBS = SW_JPT · SW_BLOCK) */
 #define SW_JPT 2
+/* keys per job per staging chunk of the key-row setup: the level kernel's
+ * staging window is SW_JPT · SW_SETUP_CH · SW_BLOCK floats (8 KB), which its
+ * level search reuses for five per-job byte arrays (5 KB) */
+#define SW_SETUP_CH 2
 
 /* SMALL: the pack kernel's context — every pack has at most SW_BLOCK active
  * jobs (one position per thread), so the 1024-position paths compile out. */
@@ -365,9 +369,10 @@ struct Ctx {
         for_jobs([&](int j, int s) { amax = sw_max(amax, jc(j, s).a); });
         A = blk.dmax(amax);
         if constexpr (ONE) {
-            /* rolled evaluation into an LDS staging window (4 keys × 4 jobs
-             * per thread per chunk), then compile-time-indexed copies */
-            constexpr int CH = 4;
+            /* rolled evaluation into an LDS staging window (SW_SETUP_CH keys
+             * × SW_JPT jobs per thread per chunk), then compile-time-indexed
+             * copies */
+            constexpr int CH = SW_SETUP_CH;
             float* stage = reinterpret_cast<float*>(sbuf);
             double prev[SW_JPT], vm[SW_JPT], ksc[SW_JPT];
             /* f(n) = a·φ(u(n)) evaluated incrementally: u(n) is nondecreasing
@@ -1419,7 +1424,7 @@ __host__ __device__ constexpr size_t sw_plan_lds_bytes(bool one) {
 __host__ __device__ constexpr size_t sw_level_lds_bytes() {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     return r16(sizeof(sw_xchg)) + r16(sizeof(double) * 3 * SW_BMAX) +
-           r16(sizeof(float) * SW_JPT * 4 * SW_BLOCK) + SW_JOB_LDS_BYTES;
+           r16(sizeof(float) * SW_JPT * SW_SETUP_CH * SW_BLOCK) + SW_JOB_LDS_BYTES;
 }
 
 /* LDS of the pack kernel: pack and repair state, counts, masks, sort exchange. */
@@ -1479,7 +1484,9 @@ __device__ __forceinline__ void level_instance(const sw_batch_dev& B, unsigned c
     }
     /* the setup's staging window; the level search's per-job bytes use the
      * same space once the key rows are in registers */
-    unsigned char* stage = carve(sizeof(float) * SW_JPT * 4 * SW_BLOCK);
+    unsigned char* stage = carve(sizeof(float) * SW_JPT * SW_SETUP_CH * SW_BLOCK);
+    static_assert(sizeof(float) * SW_JPT * SW_SETUP_CH * SW_BLOCK >= 5 * SW_LDS_JOBS,
+                  "the staging window holds the level search's five per-job byte arrays");
     c.sbuf = reinterpret_cast<uint64_t*>(stage);
     const int NJ = SW_LDS_JOBS;
     c.ncur = stage;
@@ -2176,7 +2183,7 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
 }
 
 template <int KT>
-__global__ __launch_bounds__(SW_BLOCK) void sw_level_kernel(sw_batch_dev B) {
+__global__ __launch_bounds__(SW_BLOCK, 4) void sw_level_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
     level_instance<KT>(B, sw_smem, blockIdx.x);
 }
