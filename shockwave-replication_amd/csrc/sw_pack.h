@@ -24,19 +24,43 @@
 #include "sw_block.h"
 
 #ifdef SW_STAMPS
-/* diagnostic builds: cycles per round-loop phase, thread 0's view, added
- * to swp[k] (0 setup, 1 histogram+need, 2 tiers, 3 fill, 4 tail, 5 apply) */
-#define SWP_STAMP(k)                                         \
-    do {                                                     \
-        if (threadIdx.x == 0 && swp) {                       \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
-            swp[k] += now_ - swp_t_;                         \
-            swp_t_ = now_;                                   \
-        }                                                    \
+/* diagnostic builds: cycles per round-loop phase, thread 0's view, kept in
+ * registers and added to swp[k] on exit (0 setup, 1 histogram+need, 2 tiers,
+ * 3 fill, 4 tail, 5 apply; swp[17..19] rounds, active tiers, width-tail
+ * reductions; swp[20..22] the wave loop's tier parts: head, scan, take — its
+ * "tiers" stamp then holds only the loop exits) — a global read-modify-write per stamp would add a memory
+ * round trip to every phase it times */
+#define SWP_DECL                                          \
+    uint64_t swp_t_ = __builtin_amdgcn_s_memtime();       \
+    uint64_t swp_a_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    uint32_t swp_c_[3] = {0, 0, 0}
+#define SWP_STAMP(k)                                          \
+    do {                                                      \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();   \
+        swp_a_[k] += now_ - swp_t_;                           \
+        swp_t_ = now_;                                        \
+    } while (0)
+#define SWP_COUNT(k) (swp_c_[(k) - 17] += 1)
+#define SWP_FLUSH                                                         \
+    do {                                                                  \
+        if (threadIdx.x == 0 && swp) {                                    \
+            for (int k_ = 0; k_ < 6; ++k_) swp[k_] += swp_a_[k_];         \
+            for (int k_ = 0; k_ < 3; ++k_) swp[17 + k_] += swp_c_[k_];    \
+            for (int k_ = 6; k_ < 10; ++k_) swp[14 + k_] += swp_a_[k_];   \
+        }                                                                 \
     } while (0)
 #else
+#define SWP_DECL \
+    do {         \
+    } while (0)
 #define SWP_STAMP(k) \
     do {             \
+    } while (0)
+#define SWP_COUNT(k) \
+    do {             \
+    } while (0)
+#define SWP_FLUSH \
+    do {          \
     } while (0)
 #endif
 
@@ -92,9 +116,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
     (void)swp; /* phase stamps (SW_STAMPS builds) */
     const int tid = threadIdx.x;
     const int lane = lane_id();
-#ifdef SW_STAMPS
-    uint64_t swp_t_ = __builtin_amdgcn_s_memtime();
-#endif
+    SWP_DECL;
     /* positions past A carry st = 0 (r = 0, w = 0): they fail every
      * eligibility test below, so no per-position bound check is needed */
     int32_t* Hu = L->H[0];
@@ -109,14 +131,12 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
         int32_t cap = caps ? caps[t] : G;
-#ifdef SW_STAMPS
-        if (threadIdx.x == 0 && swp) swp[17] += 1; /* rounds */
-#endif
+        SWP_COUNT(17);
         __syncthreads(); /* Hu holds the placements of round t − 1 */
         /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
          * lane m holds hv = H[m + 1] */
         const int32_t suf = wave_sufscan_i32(Hu[lane]);
-        const int32_t tailR = (R < 64 ? __shfl(suf, R, 64) : 0) + Hu[64];
+        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + Hu[64];
         const int32_t hv = (lane + 1 < R) ? Hu[lane + 1] : (lane + 1 == R ? tailR : 0);
         /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
         const int32_t S0 = wave_sufscan_i32(hv);
@@ -131,10 +151,8 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
             if (mask == 0) break;
             const int m = 63 - __builtin_clzll(mask);
-#ifdef SW_STAMPS
-            if (threadIdx.x == 0 && swp) swp[18] += 1; /* active tiers */
-#endif
-            const int32_t q = __shfl(need, m, 64) - red;
+            SWP_COUNT(18);
+            const int32_t q = __builtin_amdgcn_readlane(need, m) - red;
             int32_t lt = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
@@ -192,9 +210,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
                 best = ok ? (((E * tid + i) << 8) | (int32_t)pk_w(st[i])) : best;
             }
             best = blk.min32(best);
-#ifdef SW_STAMPS
-            if (threadIdx.x == 0 && swp) swp[19] += 1; /* width-tail reductions */
-#endif
+            SWP_COUNT(19);
             if (best == 0x7FFFFFFF) break;
             const int pos = best >> 8;
 #pragma unroll
@@ -217,5 +233,182 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
         }
         SWP_STAMP(5);
     }
+    SWP_FLUSH;
     __syncthreads();
+}
+
+/*
+ * The same round loop run by ONE wave over E1 positions per lane
+ * (position p = E1·lane + i, so a wave exclusive scan of the lane totals is
+ * again the twin's running "excl"), for instances with at most 64·E1
+ * positions.  Tier m < R tests r > m directly (min(r, R) > m is the same
+ * test when m < R).  The
+ * block version issues every scan, reduction and partial combine in all
+ * eight waves and waits at two barriers per tier; here one wave issues each
+ * step once and never waits for the others (on a C3 instance the round loop
+ * was two thirds of the pack kernel's VALU instructions).  Hu is updated by
+ * this wave alone, so its LDS atomics and reads stay in program order.
+ * Called by wave 0 only; st as in sw_pack_rounds, the round masks go to
+ * xmk[position] (LDS or workspace) with an atomic OR per placement instead
+ * of 2·E1 VGPRs held through the loop.
+ */
+template <int E1>
+__device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G, uint32_t (&st)[E1],
+                                                    uint64_t* xmk, const int32_t* caps = nullptr,
+                                                    uint64_t* swp = nullptr) {
+    (void)swp;
+    const int lane = lane_id();
+    SWP_DECL;
+    int32_t* Hu = L->H[0];
+    Hu[lane] = 0;
+    if (lane < 4) Hu[64 + lane] = 0;
+#pragma unroll
+    for (int i = 0; i < E1; ++i) xmk[E1 * lane + i] = 0;
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < E1; ++i)
+        if (st[i] != 0u) atomicAdd(&Hu[pk_r(st[i])], (int32_t)pk_w(st[i]));
+    SWP_STAMP(0);
+    for (int t = 0; t < T; ++t) {
+        const int R = T - t;
+        int32_t cap = caps ? caps[t] : G;
+        SWP_COUNT(17);
+        SWP_STAMP(9); /* diagnostic: the cost of one stamp */
+        wave_sync(); /* Hu holds the placements of round t − 1 */
+        const int32_t suf = wave_sufscan_i32(Hu[lane]);
+        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + Hu[64];
+        const int32_t hv = (lane + 1 < R) ? Hu[lane + 1] : (lane + 1 == R ? tailR : 0);
+        const int32_t S0 = wave_sufscan_i32(hv);
+        const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
+        const int32_t room = sw_pack_room(caps, t, R, G);
+        const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
+        SWP_STAMP(1);
+        int mstart = R - 1;
+        int32_t red = 0;
+        while (mstart >= 0) {
+            const uint64_t mask = __ballot(lane <= mstart && need - red > 0);
+            if (mask == 0) break;
+            const int m = 63 - __builtin_clzll(mask);
+            SWP_COUNT(18);
+            const int32_t q = __builtin_amdgcn_readlane(need, m) - red;
+            SWP_STAMP(6);
+            /* in-lane exclusive prefixes first, so the take tests of a
+             * lane's positions are independent of each other */
+            int32_t pre[E1];
+            int32_t lt = 0;
+#pragma unroll
+            for (int i = 0; i < E1; ++i) {
+                pre[i] = lt;
+                lt += (!pk_sel(st[i]) && (int)pk_r(st[i]) > m) ? (int32_t)pk_w(st[i]) : 0;
+            }
+            const int32_t base = wave_incscan_i32(lt) - lt;
+            SWP_STAMP(7);
+            int32_t took = 0;
+#pragma unroll
+            for (int i = 0; i < E1; ++i) {
+                const int32_t w = (int32_t)pk_w(st[i]);
+                const int32_t ex = base + pre[i];
+                const bool take = !pk_sel(st[i]) && (int)pk_r(st[i]) > m && ex < q && ex + w <= cap;
+                st[i] |= take ? (1u << 16) : 0u;
+                took += take ? w : 0;
+            }
+            took = wave_sum_i32(took);
+            cap -= took;
+            red += took;
+            mstart = m - 1;
+            SWP_STAMP(8);
+        }
+        SWP_STAMP(2);
+        {
+            int32_t pre[E1];
+            int32_t lt = 0;
+#pragma unroll
+            for (int i = 0; i < E1; ++i) {
+                pre[i] = lt;
+                lt += (!pk_sel(st[i]) && pk_r(st[i]) > 0) ? (int32_t)pk_w(st[i]) : 0;
+            }
+            const int32_t base = wave_incscan_i32(lt) - lt;
+            int32_t took = 0;
+#pragma unroll
+            for (int i = 0; i < E1; ++i) {
+                const int32_t w = (int32_t)pk_w(st[i]);
+                const bool take = !pk_sel(st[i]) && pk_r(st[i]) > 0 && base + pre[i] + w <= cap;
+                st[i] |= take ? (1u << 16) : 0u;
+                took += take ? w : 0;
+            }
+            cap -= wave_sum_i32(took);
+        }
+        SWP_STAMP(3);
+        while (cap > 0) {
+            int32_t best = 0x7FFFFFFF;
+#pragma unroll
+            for (int i = E1 - 1; i >= 0; --i) {
+                const bool ok = !pk_sel(st[i]) && pk_r(st[i]) > 0 && (int32_t)pk_w(st[i]) <= cap;
+                best = ok ? (((E1 * lane + i) << 8) | (int32_t)pk_w(st[i])) : best;
+            }
+            best = wave_min_i32(best);
+            SWP_COUNT(19);
+            if (best == 0x7FFFFFFF) break;
+            const int pos = best >> 8;
+#pragma unroll
+            for (int i = 0; i < E1; ++i) st[i] |= (E1 * lane + i == pos) ? (1u << 16) : 0u;
+            cap -= best & 0xFF;
+        }
+        SWP_STAMP(4);
+#pragma unroll
+        for (int i = 0; i < E1; ++i) {
+            const bool sel = pk_sel(st[i]) != 0;
+            const uint32_t r = pk_r(st[i]);
+            st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
+            if (sel) {
+                atomicAdd(&Hu[r], -(int32_t)pk_w(st[i]));
+                atomicAdd(&Hu[r - 1], (int32_t)pk_w(st[i]));
+                atomicOr((unsigned long long*)&xmk[E1 * lane + i], 1ull << t);
+            }
+        }
+        SWP_STAMP(5);
+    }
+    SWP_FLUSH;
+    wave_sync();
+}
+
+/* sw_pack_rounds for at most 512 positions, one per thread (position tid):
+ * the states are staged through LDS / workspace words xs (≥ 6 KB, free at the
+ * call) into wave 0, which runs sw_pack_rounds_wave<E1> with E1 the even
+ * number of positions per lane that covers A (2, 4, 6 or 8: a runtime bound
+ * inside the unrolled loops costs the kernel's register budget) when MULTI,
+ * else always 8 (the plan kernel, whose register file the extra copies would
+ * overflow); every thread of the block must call it. */
+template <int E1>
+__device__ __forceinline__ void sw_pack_rounds_wave_io(sw_pack_lds* L, int T, int G, uint32_t* xst,
+                                                      uint64_t* xmk, const int32_t* caps,
+                                                      uint64_t* swp) {
+    const int lane = lane_id();
+    uint32_t st[E1];
+#pragma unroll
+    for (int i = 0; i < E1; ++i) st[i] = xst[E1 * lane + i];
+    sw_pack_rounds_wave<E1>(L, T, G, st, xmk, caps, swp);
+#pragma unroll
+    for (int i = 0; i < E1; ++i) xst[E1 * lane + i] = st[i];
+}
+
+template <bool MULTI>
+__device__ __forceinline__ void sw_pack_rounds_one(sw_pack_lds* L, int A, int T, int G, uint32_t& st1,
+                                                   uint64_t& mk1, uint64_t* xs,
+                                                   const int32_t* caps = nullptr,
+                                                   uint64_t* swp = nullptr) {
+    uint32_t* xst = reinterpret_cast<uint32_t*>(xs);
+    uint64_t* xmk = xs + SW_BLOCK / 2;
+    xst[threadIdx.x] = st1; /* 0 past A */
+    __syncthreads();
+    if (wave_id() == 0) {
+        if (!MULTI) sw_pack_rounds_wave_io<8>(L, T, G, xst, xmk, caps, swp);
+        else if (A <= 128) sw_pack_rounds_wave_io<2>(L, T, G, xst, xmk, caps, swp);
+        else if (A <= 256) sw_pack_rounds_wave_io<4>(L, T, G, xst, xmk, caps, swp);
+        else if (A <= 384) sw_pack_rounds_wave_io<6>(L, T, G, xst, xmk, caps, swp);
+        else sw_pack_rounds_wave_io<8>(L, T, G, xst, xmk, caps, swp);
+    }
+    __syncthreads();
+    st1 = xst[threadIdx.x];
+    mk1 = xmk[threadIdx.x];
 }

@@ -56,6 +56,8 @@ def main():
         pnames = ["setup", "hist+need", "tiers", "fill", "tail", "apply"]
         print("   pack round loop (all packs of an instance):",
               " ".join(f"{n} {pk[:, i].mean():.0f}" for i, n in enumerate(pnames)))
+        print("   wave round loop tier parts: head {:.0f} scan {:.0f} take {:.0f} | one stamp {:.0f}".format(
+            *st_all[:, 28:31].mean(axis=0), st_all[:, 31].mean() / max(rounds, 1)))
         print(f"   sorts (all packs): {srt.mean():.0f}; rounds {rounds:.1f}, active tiers {scans:.1f}, "
               f"width-tail reductions {misses:.1f}")
         lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
