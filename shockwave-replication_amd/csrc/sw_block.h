@@ -136,6 +136,19 @@ __device__ __forceinline__ double wave_max_f64(double v) {
     return __builtin_bit_cast(double, sw_readlane63_u64(x));
 }
 
+/* min of doubles (identity +inf) */
+__device__ __forceinline__ double wave_min_f64(double v) {
+    uint64_t x = __builtin_bit_cast(uint64_t, v);
+#define SW_MIND_(c, rm)                                                       \
+    {                                                                         \
+        const uint64_t y_ = SW_DPP64(x, 0x7FF0000000000000ull, c, rm);        \
+        x = __builtin_bit_cast(double, y_) < __builtin_bit_cast(double, x) ? y_ : x; \
+    }
+    SW_DPP64_STEPS(SW_MIND_)
+#undef SW_MIND_
+    return __builtin_bit_cast(double, sw_readlane63_u64(x));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -59,14 +59,13 @@ namespace {
 #ifdef SW_STAMPS
 /* level-search breakdown (thread 0's view), slots 16 + k: 0 force pass,
  * 1 price probes, 2 tie group, 3 width tail, 4 evaluation, 5 M_lo search,
- * 6 levels_between */
+ * 6 levels_between; 7 / 8 count price probes / M_lo passes.  Accumulated in
+ * registers (lsa) and added to the slots when the search returns. */
 #define LS_STAMP(k)                                            \
     do {                                                       \
-        if (threadIdx.x == 0 && lsp) {                         \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
-            lsp[k] += now_ - ls_t;                             \
-            ls_t = now_;                                       \
-        }                                                      \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();    \
+        lsa[k] += now_ - ls_t;                                 \
+        ls_t = now_;                                           \
     } while (0)
 #else
 #define LS_STAMP(k) \
@@ -146,6 +145,7 @@ struct Ctx {
     uint64_t* swp; /* pack phase stamps of this instance */
     uint64_t* lsp; /* level-search stamps */
     uint64_t ls_t;
+    uint64_t lsa[9];
 #endif
     /* per-job state (LDS when ONE, HBM workspace otherwise) */
     uint8_t *ncur, *lcur, *tkcur, *nbest, *placed, *placed2, *nfin;
@@ -517,7 +517,7 @@ struct Ctx {
                     wg = blk.sum32_max_min(wg, mx, mn, MX, MN);
                     passes++;
 #ifdef SW_STAMPS
-                    if (threadIdx.x == 0 && lsp) lsp[7] += 1; /* price probes */
+                    lsa[7] += 1; /* price probes */
 #endif
                     const bool down = wg <= bud;
 #pragma unroll
@@ -662,6 +662,7 @@ struct Ctx {
     __device__ __forceinline__ double level_search() {
 #ifdef SW_STAMPS
         ls_t = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < 9; ++k) lsa[k] = 0;
 #endif
         SelEval best, e1, e2, elo;
         best.U = best.Mact = best.ubound = 0.0;
@@ -712,7 +713,7 @@ struct Ctx {
                 blk.sum_max_min(f, bmx, bmn, F, BMX, BMN);
                 passes++;
 #ifdef SW_STAMPS
-                if (threadIdx.x == 0 && lsp) lsp[8] += 1; /* M_lo passes */
+                lsa[8] += 1; /* M_lo passes */
 #endif
                 if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
                 else { lo = BMN <= hi ? BMN : hi; Fb = F; }
@@ -801,6 +802,10 @@ struct Ctx {
         }
         lsU = best.U;
         lsM = best.Mact;
+#ifdef SW_STAMPS
+        if (threadIdx.x == 0 && lsp)
+            for (int k = 0; k < 9; ++k) lsp[k] += lsa[k];
+#endif
         __syncthreads();
         return ret;
     }

@@ -11,11 +11,11 @@
  * and-not / ctz / clz word operations.  Edge costs W[t][u] are built by all
  * threads, one (t, u) pair per thread, once per load size F and afterwards
  * only in the rows and columns of the rounds a cancelled cycle touched (the
- * other entries cannot change).  Bellman–Ford is block-wide: waves 0–3 relax
- * a quarter of the source rounds each (lane = target round), wave 0 combines
- * them, handles the free-capacity node V as a wave-uniform scalar and checks
- * the predecessor graph by pointer doubling (7 shuffles reach 128 ≥ T + 1
- * steps); each load size's runs start from its previous run's distances.  A
+ * other entries cannot change).  Bellman–Ford is block-wide: the eight waves
+ * relax an eighth of the source rounds each (lane = target round), wave 0
+ * combines them, handles the free-capacity node V as a wave-uniform scalar
+ * and checks the predecessor graph by pointer doubling (⌈log2(T + 1)⌉
+ * shuffles); each load size's runs start from its previous run's distances.  A
  * cycle's moves are applied with LDS atomics.
  */
 #pragma once
@@ -52,11 +52,11 @@ struct sw_p2x_lds {
     int32_t cyc[SW_TMAX + 2];
     double delta;
     /* block-wide Bellman–Ford: distances and predecessors (V at index T),
-     * the four relaxing waves' partial minima, the loop's exit flag */
+     * each wave's partial minima over its rows, the loop's exit flag */
     double bd[SW_TMAX + 1];
     int32_t bp[SW_TMAX + 1];
-    double pv[4][64];
-    int32_t pt[4][64];
+    double pv[SW_WAVES][64];
+    int8_t pt[SW_WAVES][64];
     int32_t bfdone;
     int32_t fq[SW_P2X_KMAX]; /* F / w_k for the current load size (0: w_k ∤ F) */
     double dw[SW_P2X_KMAX][SW_TMAX + 1]; /* each load size's last Bellman–Ford distances */
@@ -83,27 +83,28 @@ static __device__ __forceinline__ int p2x_class(const sw_p2x_lds* L, int32_t w) 
 }
 
 /* Bellman–Ford of oracle/p2x_twin.c find_cycle, block-wide: each sweep,
- * waves 0–3 relax one quarter of the source rounds each (lane u = target
- * round u: the smallest d[t] + W[t][u] of the quarter and its first t, read
- * against the distances in LDS), then wave 0 combines the quarters in round
+ * every wave relaxes ⌈T / 8⌉ consecutive source rounds (lane u = target
+ * round u: the smallest d[t] + W[t][u] of its rows and their first t, read
+ * against the distances in LDS), then wave 0 combines the eight in round
  * order (strict <: the sequential scan's answer), adds V (a wave-uniform
- * scalar), publishes the new distances and, after the odd sweeps and the
- * last, checks the predecessor graph for a cycle by pointer doubling
- * (7 shuffles reach 128 ≥ T + 1 steps).  Leaves the cycle in L->cyc / L->len
- * (0: none).  All threads call it. */
+ * scalar; its minimum by a DPP reduction), publishes the new distances and,
+ * after the odd sweeps and the last, checks the predecessor graph for a
+ * cycle by pointer doubling: 2^⌈log2(T + 1)⌉ ≥ T + 1 steps from a vertex are
+ * still defined exactly when its walk enters a cycle, and the lowest such
+ * vertex reaches the same cycle as the twin's walk from it.  Leaves the
+ * cycle in L->cyc / L->len (0: none).  All threads call it. */
 static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const double* W, int T, int F,
-                                                      double* dw, bool warm, uint64_t* sp = nullptr) {
+                                                      double* dw, bool warm, uint64_t (&acc)[11]) {
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    (void)sp;
+    (void)acc;
 #ifdef SW_STAMPS
+    /* stamps accumulate in the caller's registers (acc, sw_p2x_block's) */
     uint64_t bt_ = __builtin_amdgcn_s_memtime();
 #define BF_STAMP(k)                                                   \
     do {                                                              \
-        if (tid == 0 && sp) {                                         \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime();       \
-            sp[k] += now_ - bt_;                                      \
-            bt_ = now_;                                               \
-        }                                                             \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();           \
+        acc[k] += now_ - bt_;                                         \
+        bt_ = now_;                                                   \
     } while (0)
 #else
 #define BF_STAMP(k) \
@@ -118,14 +119,16 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
     if (tid == 0) L->bfdone = 0;
     const bool roomok = wv == 0 && act && L->room[lane] >= F;
     const bool anyroom = __ballot(roomok) != 0; /* else V has no in-edge: it never changes */
-    const int nq = (T + 3) >> 2;
+    const int nq = (T + SW_WAVES - 1) / SW_WAVES; /* rows per relaxing wave */
+    int ndbl = 0; /* pointer doublings: 2^ndbl ≥ T + 1 steps */
+    while ((1 << ndbl) < T + 1) ++ndbl;
     __syncthreads();
     for (int it = 0; it <= T; ++it) {
 #ifdef SW_STAMPS
-        if (tid == 0 && sp) sp[7] += 1;
+        acc[7] += 1;
 #endif
         BF_STAMP(10);
-        if (wv < 4) {
+        {
             /* W[t][t] and missing edges are SW_P2X_NONE and every distance is
              * ≤ 0, so they never win: no per-edge tests */
             const int ul = act ? lane : 0;
@@ -139,7 +142,7 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
                 ct = take ? t : ct;
             }
             L->pv[wv][lane] = cb;
-            L->pt[wv][lane] = ct;
+            L->pt[wv][lane] = (int8_t)ct;
         }
         __syncthreads();
         BF_STAMP(9);
@@ -151,7 +154,7 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
             double cb = L->pv[0][lane];
             int ct = L->pt[0][lane];
 #pragma unroll
-            for (int q = 1; q < 4; ++q) {
+            for (int q = 1; q < SW_WAVES; ++q) {
                 const double v = L->pv[q][lane];
                 const bool take = q * nq < T && v < cb;
                 cb = take ? v : cb;
@@ -172,7 +175,7 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
             double m = dV;
             uint64_t at = 0;
             if (anyroom) {
-                m = wave_min(roomok ? d : SW_P2X_NONE);
+                m = wave_min_f64(roomok ? d : SW_P2X_NONE);
                 at = __ballot(roomok && d == m);
                 vbetter = m < dV;
             }
@@ -198,16 +201,20 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
                  * exist yet; from warm distances also after the first) */
                 if ((it & 1) || it == T || (warm && it == 0)) {
                     int y = act ? pr : -1, yV = prV;
-                    for (int s2 = 0; s2 < 7; ++s2) {
+#pragma unroll
+                    for (int s2 = 0; s2 < 7; ++s2) { /* 2^7 > SW_TMAX */
+                        if (s2 >= ndbl) break;
                         const int g = __shfl(y, (y >= 0 && y < T) ? y : 0, 64);
-                        const int gV = (yV >= 0 && yV < T) ? __shfl(y, yV, 64) : (yV == T ? yV : -1);
+                        /* yV (V's walk) is wave-uniform: a lane read, not a shuffle */
+                        const int gV = (yV >= 0 && yV < T) ? __builtin_amdgcn_readlane(y, yV)
+                                                           : (yV == T ? yV : -1);
                         y = y < 0 ? -1 : (y == T ? yV : g);
                         yV = gV;
                     }
                     const uint64_t cbits = __ballot(act && y >= 0);
                     if (cbits) {
                         done = 1;
-                        const int y0 = __shfl(y, (int)__builtin_ctzll(cbits), 64);
+                        const int y0 = __builtin_amdgcn_readlane(y, (int)__builtin_ctzll(cbits));
                         if (act) L->pr[lane] = pr;
                         if (lane == 0) L->pr[T] = prV;
                         wave_sync();
@@ -240,94 +247,100 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
 }
 
 /* sw_p2x_cost (sw_p2x.h) for classes of at most 256 jobs (≤ 4 words) and
- * q ≤ 4, branch-free: the and-not words are loaded once, listed in scan order
- * (ascending words for u < t, descending otherwise), and each of the q picks
- * takes the first set bit (lowest, or highest when descending) of the first
- * non-empty word with selects only; the c loads are then issued together and
- * summed in selection order (the same sum).  Other cases: sw_p2x_cost. */
-static __device__ __forceinline__ double p2x_cost_dev(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
+ * q ≤ 4, for one direction (LO: u < t, ascending ranks; else descending):
+ * the and-not words are loaded in scan order (the word count nw and q are
+ * uniform over the wave, so the loads and the pick loop have no per-lane
+ * selects), and each pick takes the first set bit (lowest, or highest) of
+ * the first non-empty word; c is summed in selection order from 0.0, as the
+ * twin does.  Other cases: sw_p2x_cost. */
+template <bool LO>
+static __device__ __forceinline__ double p2x_cost_dir(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
                                                       int q, int t, int u, const double* c) {
     if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, ws, q, t, u, c);
-    const bool lo = u < t;
-    uint64_t x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = i < nw ? (Bt[i * ws] & ~Bu[i * ws]) : 0ull;
-    /* y[s] = the s-th word in scan order */
     uint64_t y[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const int i = lo ? s : nw - 1 - s;
-        y[s] = (i >= 0 && i < 4) ? (i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]) : 0ull;
+        const int i = LO ? s : nw - 1 - s;
+        y[s] = s < nw ? (Bt[i * ws] & ~Bu[i * ws]) : 0ull;
     }
     const int avail = __popcll(y[0]) + __popcll(y[1]) + __popcll(y[2]) + __popcll(y[3]);
     if (avail < q) return SW_P2X_NONE;
-    int rk[4];
+    double sum = 0.0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
+        if (g >= q) break;
         const int s = y[0] ? 0 : y[1] ? 1 : y[2] ? 2 : 3;
         const uint64_t ys = s == 0 ? y[0] : s == 1 ? y[1] : s == 2 ? y[2] : y[3];
-        const int b = lo ? __builtin_ctzll(ys) : 63 - __builtin_clzll(ys);
-        rk[g] = 64 * (lo ? s : nw - 1 - s) + (b & 63);
-        const uint64_t cl = ys & ~(1ull << (b & 63));
+        const int b = LO ? __builtin_ctzll(ys) : 63 - __builtin_clzll(ys);
+        const uint64_t cl = LO ? (ys & (ys - 1)) : (ys & ~(1ull << (b & 63)));
         y[0] = s == 0 ? cl : y[0];
         y[1] = s == 1 ? cl : y[1];
         y[2] = s == 2 ? cl : y[2];
         y[3] = s == 3 ? cl : y[3];
+        sum = sum + c[64 * (LO ? s : nw - 1 - s) + (b & 63)];
     }
-    double cv[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) cv[g] = c[g < q ? rk[g] : rk[0]];
-    double sum = cv[0];
-#pragma unroll
-    for (int g = 1; g < 4; ++g) sum = g < q ? sum + cv[g] : sum;
     return sum * (double)(u - t);
 }
 
 /* W entries for load size F: every entry (all = true) or those in a row or
  * column of L->touched.  L->fq[k] = F / w_k for the classes that can carry F
  * (w_k | F), 0 for the others: set once per load size, so the per-entry loop
- * has no integer divisions. */
+ * has no integer divisions.  The T(T − 1) off-diagonal pairs are walked as
+ * two triangles, all u < t first, so every wave but one has a single move
+ * direction (one code path of p2x_cost_dir); pair i of a triangle is (a, b),
+ * b < a, with a(a − 1)/2 ≤ i < a(a + 1)/2. */
 template <int NT>
 static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const uint64_t* B, const double* pc,
                                                    double* W, int8_t* Wk, int T, double delta, bool all) {
     const uint64_t tm = L->touched;
     const int K = L->K;
-    for (int e = threadIdx.x; e < T * T; e += NT) {
-        const int t = e / T, u = e - t * T;
+    const int P = T * (T - 1) / 2;
+    if (all)
+        for (int t = threadIdx.x; t < T; t += NT) {
+            W[t * T + t] = SW_P2X_NONE;
+            Wk[t * T + t] = (int8_t)-1;
+        }
+    for (int e = threadIdx.x; e < 2 * P; e += NT) {
+        const bool lo = e < P;
+        const int i = lo ? e : e - P;
+        int a = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)i)) * 0.5f);
+        if (a * (a - 1) / 2 > i) --a;
+        if ((a + 1) * a / 2 <= i) ++a;
+        const int b = i - a * (a - 1) / 2;
+        const int t = lo ? a : b, u = lo ? b : a;
         if (!all && !(((tm >> t) | (tm >> u)) & 1ull)) continue;
         double best = SW_P2X_NONE;
         int bk = -1;
-        if (t != u) {
 #pragma unroll 1
-            for (int k = 0; k < K; ++k) {
-                const int q = L->fq[k];
-                if (q == 0) continue;
-                const int nw = L->nw[k];
-                const uint64_t* Bk = B + L->boff[k]; /* word-major: word w of round t at w·T + t */
-                const double cost = p2x_cost_dev(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k]);
-                if (cost < best) {
-                    best = cost;
-                    bk = k;
-                }
+        for (int k = 0; k < K; ++k) {
+            const int q = L->fq[k];
+            if (q == 0) continue;
+            const int nw = L->nw[k];
+            const uint64_t* Bk = B + L->boff[k]; /* word-major: word w of round t at w·T + t */
+            const double cost = lo ? p2x_cost_dir<true>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k])
+                                   : p2x_cost_dir<false>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k]);
+            if (cost < best) {
+                best = cost;
+                bk = k;
             }
         }
-        W[e] = bk >= 0 ? best + delta : SW_P2X_NONE;
-        Wk[e] = (int8_t)bk;
+        W[t * T + u] = bk >= 0 ? best + delta : SW_P2X_NONE;
+        Wk[t * T + u] = (int8_t)bk;
     }
 }
 
-/* diagnostic builds (SW_STAMPS): thread 0 adds cycles to sp[k]: 0 classes,
- * 1 ranks, 2 bitsets and δ, 3 edge builds, 4 Bellman–Ford, 5 selecting a
- * cycle's moves, 6 applying them; counts: 7 Bellman–Ford sweeps, 8 edge
- * builds; inside Bellman–Ford: 9 relaxations, 10 predecessor walks */
+/* diagnostic builds (SW_STAMPS): thread 0's cycles, accumulated in registers
+ * (sp_a_) and added to sp[k] on return — a global read-modify-write per stamp
+ * would add a memory round trip to each phase it times: 0 classes, 1 ranks,
+ * 2 bitsets and δ, 3 edge builds, 4 Bellman–Ford, 5 selecting a cycle's
+ * moves, 6 applying them; counts: 7 Bellman–Ford sweeps, 8 edge builds;
+ * inside Bellman–Ford: 9 relaxations, 10 predecessor walks */
 #ifdef SW_STAMPS
 #define P2X_STAMP(k)                                                 \
     do {                                                             \
-        if (threadIdx.x == 0 && sp) {                                \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
-            sp[k] += now_ - sp_t_;                                   \
-            sp_t_ = now_;                                            \
-        }                                                            \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();          \
+        sp_a_[k] += now_ - sp_t_;                                    \
+        sp_t_ = now_;                                                \
     } while (0)
 #else
 #define P2X_STAMP(k) \
@@ -416,6 +429,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     constexpr int NT = NW * 64;
     const int tid = threadIdx.x;
     (void)sp;
+    uint64_t sp_a_[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef SW_STAMPS
     uint64_t sp_t_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -673,10 +687,8 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                 p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
                 __syncthreads();
                 P2X_STAMP(3);
-#ifdef SW_STAMPS
-                if (threadIdx.x == 0 && sp) sp[8] += 1;
-#endif
-                p2x_find_cycle(L, W, T, F, L->dw[ki], ((havem >> ki) & 1u) != 0, sp);
+                sp_a_[8] += 1;
+                p2x_find_cycle(L, W, T, F, L->dw[ki], ((havem >> ki) & 1u) != 0, sp_a_);
                 havem |= 1u << ki;
                 P2X_STAMP(4);
                 const int len = L->len;
@@ -752,5 +764,9 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             }
         }
     }
+#ifdef SW_STAMPS
+    if (threadIdx.x == 0 && sp)
+        for (int k = 0; k < 11; ++k) sp[k] += sp_a_[k];
+#endif
     return ncancel;
 }
