@@ -33,6 +33,21 @@ using sw_xchg = sw_xchg_t<SW_WAVES>;
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
+/* Block-reduction results are workgroup-uniform: they are returned through
+ * v_readfirstlane so that the compiler keeps them (and what is derived from
+ * them) in SGPRs instead of VGPRs — in the register-capped kernels uniform
+ * state held per lane was spilled to scratch. */
+__device__ __forceinline__ int32_t sw_u32(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t sw_u64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int64_t sw_i64(int64_t x) { return (int64_t)sw_u64((uint64_t)x); }
+__device__ __forceinline__ double sw_f64u(double x) {
+    return __builtin_bit_cast(double, sw_u64(__builtin_bit_cast(uint64_t, x)));
+}
+
 /* Order LDS accesses of one wave (the hardware keeps a wave's LDS ops in
  * order; this keeps the compiler from moving them). */
 __device__ __forceinline__ void wave_sync() {
@@ -266,7 +281,7 @@ struct sw_blk_t {
 #pragma unroll
         for (int w = 0; w < NW; ++w) t += X->s[par][w];
         flip();
-        return t;
+        return sw_u32(t);
     }
 
     __device__ __forceinline__ int32_t min32(int32_t v) {
@@ -277,7 +292,7 @@ struct sw_blk_t {
 #pragma unroll
         for (int w = 1; w < NW; ++w) t = X->s[par][w] < t ? X->s[par][w] : t;
         flip();
-        return t;
+        return sw_u32(t);
     }
 
     /* 64-bit sums of values that fit in 32 bits per wave (all callers sum
@@ -290,7 +305,7 @@ struct sw_blk_t {
 #pragma unroll
         for (int k = 0; k < NW; ++k) t += X->i[par][k][0];
         flip();
-        return t;
+        return sw_i64(t);
     }
 
     __device__ __forceinline__ void sum2(int64_t a, int64_t b, int64_t& ra, int64_t& rb) {
@@ -302,8 +317,8 @@ struct sw_blk_t {
 #pragma unroll
         for (int w = 0; w < NW; ++w) { ta += X->i[par][w][0]; tb += X->i[par][w][1]; }
         flip();
-        ra = ta;
-        rb = tb;
+        ra = sw_i64(ta);
+        rb = sw_i64(tb);
     }
 
     __device__ __forceinline__ uint64_t umax(uint64_t v) {
@@ -314,7 +329,7 @@ struct sw_blk_t {
 #pragma unroll
         for (int w = 0; w < NW; ++w) m = X->u[par][w] > m ? X->u[par][w] : m;
         flip();
-        return m;
+        return sw_u64(m);
     }
 
     __device__ __forceinline__ double dmax(double v) {
@@ -325,7 +340,7 @@ struct sw_blk_t {
 #pragma unroll
         for (int w = 1; w < NW; ++w) m = X->d[par][w][0] > m ? X->d[par][w][0] : m;
         flip();
-        return m;
+        return sw_f64u(m);
     }
 
     /* Σ v (fits 32 bits per wave), max mx and min mn, one barrier. */
@@ -349,9 +364,9 @@ struct sw_blk_t {
             b = X->u2[par][k][1] < b ? X->u2[par][k][1] : b;
         }
         flip();
-        S = t;
-        MX = a;
-        MN = b;
+        S = sw_i64(t);
+        MX = sw_u64(a);
+        MN = sw_u64(b);
     }
 
     /* Σ v, max mx and min mn of non-negative 32-bit values, one barrier
@@ -377,9 +392,9 @@ struct sw_blk_t {
             b = pn < b ? pn : b;
         }
         flip();
-        MX = a;
-        MN = b;
-        return t;
+        MX = sw_u32(a);
+        MN = sw_u32(b);
+        return sw_u32(t);
     }
 
     /* sw_detsum of the per-thread partials v, and the max of m, together. */
@@ -400,8 +415,8 @@ struct sw_blk_t {
 #pragma unroll
             for (int i = 0; i < h; ++i) s[i] = s[i] + s[i + h];
         flip();
-        S = s[0];
-        M = mm;
+        S = sw_f64u(s[0]);
+        M = sw_f64u(mm);
     }
 
     /* sw_detsum of a and of b, the max of m ≥ 0 and the sum of the small
@@ -438,10 +453,10 @@ struct sw_blk_t {
                 sb[i] = sb[i] + sb[i + h];
             }
         flip();
-        SA = sa[0];
-        SB = sb[0];
-        M = mm;
-        C = t;
+        SA = sw_f64u(sa[0]);
+        SB = sw_f64u(sb[0]);
+        M = sw_f64u(mm);
+        C = sw_i64(t);
     }
 
     __device__ __forceinline__ double detsum(double v) {
@@ -463,7 +478,7 @@ struct sw_blk_t {
             tot += t;
         }
         flip();
-        total = tot;
+        total = sw_u32(tot);
         return base + x - v;
     }
 };

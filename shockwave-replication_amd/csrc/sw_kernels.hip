@@ -78,6 +78,23 @@ struct SelEval {
     uint32_t rho; /* price ρ* bits of the level (0 when every item fits) */
 };
 
+/* Workgroup-uniform values (block-reduction results and what the level
+ * search derives from them) moved to SGPRs: held in VGPRs, the level
+ * search's four evaluations and its bracket took ~40 VGPRs of uniform data,
+ * which the 128-VGPR level kernel spilled to scratch — 2.6 GB of scratch
+ * write-backs per 32768-instance launch (profiles/r6z1_summary.json). */
+__device__ __forceinline__ double sw_uni(double x) { return sw_f64u(x); }
+__device__ __forceinline__ uint32_t sw_uni(uint32_t x) { return (uint32_t)sw_u32((int32_t)x); }
+__device__ __forceinline__ SelEval sw_uni(const SelEval& e) {
+    SelEval r;
+    r.U = sw_uni(e.U);
+    r.Mact = sw_uni(e.Mact);
+    r.J = sw_uni(e.J);
+    r.ubound = sw_uni(e.ubound);
+    r.rho = sw_uni(e.rho);
+    return r;
+}
+
 /* packed per-position packer state: r | w << 8 | sel << 16 */
 __device__ __forceinline__ uint32_t st_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t st_w(uint32_t s) { return (s >> 8) & 0xFFu; }
@@ -718,7 +735,7 @@ struct Ctx {
                 if (F <= C) { hi = BMX >= lo ? BMX : lo; Fh = F; }
                 else { lo = BMN <= hi ? BMN : hi; Fb = F; }
             }
-            M_lo = sw_from_bits(lo);
+            M_lo = sw_uni(sw_from_bits(lo));
             LS_STAMP(5);
         }
         int phase = levels ? 1 : 0, it = 0;
@@ -727,7 +744,7 @@ struct Ctx {
             if (phase == 1) M = M_lo;
             else if (phase == 2 || phase == 4) M = m1;
             else if (phase >= 3) M = m2;
-            const SelEval ev = select_level(M, phase == 0, plo, phi);
+            const SelEval ev = sw_uni(select_level(M, phase == 0, plo, phi));
             if (phase == 1) {
                 best = ev;
                 elo = ev;
@@ -738,8 +755,8 @@ struct Ctx {
                 for_jobs([&](int j, int s) { um = um + fval(j, s, Tj(j, s)); });
                 const double U_max = blk.detsum(um);
                 passes++;
-                const double wmax = (U_max - ev.U) / k;
-                ret = ev.ubound - k * M_lo;
+                const double wmax = sw_uni((U_max - ev.U) / k);
+                ret = sw_uni(ev.ubound - k * M_lo);
                 if (!(wmax > 0.0)) break;
                 if (levels_between(M_lo, M_lo + wmax) == 0) break;
                 plo = 0;
@@ -751,21 +768,21 @@ struct Ctx {
                 if (!levels) { /* no makespan term: the utility optimum */
                     best = ev;
                     for_jobs([&](int j, int s) { (void)s; nbest[j] = ncur[j]; });
-                    ret = ev.ubound - k * ev.Mact;
+                    ret = sw_uni(ev.ubound - k * ev.Mact);
                     break;
                 }
                 keep_best(ev, best);
-                ret = ev.ubound - k * M_lo;
+                ret = sw_uni(ev.ubound - k * M_lo);
                 const double width = (ev.U - elo.U) / k;
                 a = M_lo;
-                b = sw_min(ev.Mact, M_lo + width);
+                b = sw_uni(sw_min(ev.Mact, M_lo + width));
                 ra = elo.rho;
                 rb = ev.rho;
                 it = 0;
                 if (!(a < b)) break;
                 if (levels_between(a, b) == 0) break;
-                m1 = a + (b - a) * SW_GS_A;
-                m2 = a + (b - a) * SW_GS_B;
+                m1 = sw_uni(a + (b - a) * SW_GS_A);
+                m2 = sw_uni(a + (b - a) * SW_GS_B);
                 plo = rb;
                 phi = ra;
                 phase = 2;
@@ -789,12 +806,12 @@ struct Ctx {
             if (!(a < b)) break;
             if (levels_between(a, b) == 0) break;
             if (left) {
-                m1 = a + (b - a) * SW_GS_A;
+                m1 = sw_uni(a + (b - a) * SW_GS_A);
                 plo = e2.rho;
                 phi = ra;
                 phase = 4;
             } else {
-                m2 = a + (b - a) * SW_GS_B;
+                m2 = sw_uni(a + (b - a) * SW_GS_B);
                 plo = rb;
                 phi = e1.rho;
                 phase = 5;

@@ -6,7 +6,7 @@ TAG=${1:-quick}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 100 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/bench_c3.json 2> $OUT/bench_c3.err &&
 timeout -k 10 120 python -u bench.py --workload c4 --steps 20 --warmup 3 > $OUT/bench_c4.json 2> $OUT/bench_c4.err &&
 timeout -k 10 120 python -u tools/stamps.py 256 > $OUT/stamps.log 2>&1
