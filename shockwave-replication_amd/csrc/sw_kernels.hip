@@ -1127,17 +1127,15 @@ struct Ctx {
                 const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp1];
                 uint32_t st1[1] = {mine ? ((uint32_t)nin[jp1] | (wq << 8)) : 0u};
                 uint64_t mk1[1] = {0ull};
-                /* the pack kernel runs the round loop in wave 0
-                 * (sw_pack_rounds_one; the sort is done with sbuf, whose
-                 * first 6 KB stage the states); the plan kernel keeps the
-                 * block form, as the wave form's registers would spill its
-                 * full register file — except in diagnostic builds, whose
-                 * stamps time the pack kernel's form */
+                /* the round loop in wave 0 (sw_pack_rounds_one; the sort is
+                 * done with sbuf, whose first 6 KB stage the states): the
+                 * pack kernel sizes it by A, the plan kernel takes the
+                 * 8-position form only (its register file has no room for
+                 * four copies) */
 #ifdef SW_STAMPS
                 sw_pack_rounds_one<SMALL>(PL, A_, T, G, st1[0], mk1[0], sbuf, capsp, swp);
 #else
-                if constexpr (SMALL) sw_pack_rounds_one<true>(PL, A_, T, G, st1[0], mk1[0], sbuf, capsp);
-                else sw_pack_rounds<1>(blk, PL, A_, T, G, st1, mk1, capsp);
+                sw_pack_rounds_one<SMALL>(PL, A_, T, G, st1[0], mk1[0], sbuf, capsp);
 #endif
                 for_jobs([&](int j, int s) {
                     (void)s;
