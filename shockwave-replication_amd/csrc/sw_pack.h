@@ -73,6 +73,11 @@ __device__ __forceinline__ uint32_t pk_sel(uint32_t s) { return (s >> 16) & 1u; 
 struct sw_pack_lds {
     int32_t H[2][68];
     int32_t SH[2][68];
+    /* the one-wave loop's histogram, in 8 copies by lane & 7: the positions a
+     * round places mostly share one or two remaining-round counts, and their
+     * atomics on one bin serialised in the LDS (copy c's bin v sits in bank
+     * 8c + v, so the copies of a bin never share a bank) */
+    int32_t Hc[8][72];
 };
 
 /*
@@ -246,8 +251,9 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
  * block version issues every scan, reduction and partial combine in all
  * eight waves and waits at two barriers per tier; here one wave issues each
  * step once and never waits for the others (on a C3 instance the round loop
- * was two thirds of the pack kernel's VALU instructions).  Hu is updated by
- * this wave alone, so its LDS atomics and reads stay in program order.
+ * was two thirds of the pack kernel's VALU instructions).  The histogram
+ * (L->Hc, eight copies summed at each round's start) is updated by this wave
+ * alone, so its LDS atomics and reads stay in program order.
  * Called by wave 0 only; st as in sw_pack_rounds, the round masks go to
  * xmk[position] (LDS or workspace) with an atomic OR per placement instead
  * of 2·E1 VGPRs held through the loop.
@@ -259,25 +265,35 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
     (void)swp;
     const int lane = lane_id();
     SWP_DECL;
-    int32_t* Hu = L->H[0];
-    Hu[lane] = 0;
-    if (lane < 4) Hu[64 + lane] = 0;
+    int32_t* Hm = L->Hc[lane & 7]; /* this lane's histogram copy */
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        L->Hc[c][lane] = 0;
+        if (lane < 8) L->Hc[c][64 + lane] = 0;
+    }
 #pragma unroll
     for (int i = 0; i < E1; ++i) xmk[E1 * lane + i] = 0;
     wave_sync();
 #pragma unroll
     for (int i = 0; i < E1; ++i)
-        if (st[i] != 0u) atomicAdd(&Hu[pk_r(st[i])], (int32_t)pk_w(st[i]));
+        if (st[i] != 0u) atomicAdd(&Hm[pk_r(st[i])], (int32_t)pk_w(st[i]));
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
         int32_t cap = caps ? caps[t] : G;
         SWP_COUNT(17);
         SWP_STAMP(9); /* diagnostic: the cost of one stamp */
-        wave_sync(); /* Hu holds the placements of round t − 1 */
-        const int32_t suf = wave_sufscan_i32(Hu[lane]);
-        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + Hu[64];
-        const int32_t hv = (lane + 1 < R) ? Hu[lane + 1] : (lane + 1 == R ? tailR : 0);
+        wave_sync(); /* the copies hold the placements of round t − 1 */
+        int32_t h0 = 0, h1 = 0; /* bins lane and lane + 1, the copies summed */
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            h0 += L->Hc[c][lane];
+            h1 += L->Hc[c][lane + 1];
+        }
+        const int32_t h64 = __builtin_amdgcn_readlane(h1, 63);
+        const int32_t suf = wave_sufscan_i32(h0);
+        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + h64;
+        const int32_t hv = (lane + 1 < R) ? h1 : (lane + 1 == R ? tailR : 0);
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
         const int32_t room = sw_pack_room(caps, t, R, G);
@@ -361,8 +377,8 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
             const uint32_t r = pk_r(st[i]);
             st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
             if (sel) {
-                atomicAdd(&Hu[r], -(int32_t)pk_w(st[i]));
-                atomicAdd(&Hu[r - 1], (int32_t)pk_w(st[i]));
+                atomicAdd(&Hm[r], -(int32_t)pk_w(st[i]));
+                atomicAdd(&Hm[r - 1], (int32_t)pk_w(st[i]));
                 atomicOr((unsigned long long*)&xmk[E1 * lane + i], 1ull << t);
             }
         }
