@@ -98,10 +98,12 @@ def main():
             s0 += 1
     s = sn.Solver(device=0)
     bad = 0
+    iters = []  # (passes, seed, N, T, G, k): the search's pass count per instance
     for c0 in range(0, n, chunk):
         probs = [fz.fuzz_problem(i) for i in seeds[c0:c0 + chunk]]
         rb = [s.solve(a) for a in probs] if single else s.solve_batch(probs)
         for i, (a, r) in enumerate(zip(probs, rb)):
+            iters.append((int(r["iters"]), seeds[c0 + i], a.N, a.T, a.G, float(a.k)))
             d = diff(r, twin(a))
             if d:
                 bad += 1
@@ -111,6 +113,12 @@ def main():
             print(f"... {c0 + chunk} solved, {bad} differ", flush=True)
     form = "single" if single else f"batched by {chunk}" + (" (on-chip)" if "--onchip" in sys.argv else "")
     print(f"{bad} of {n} differ ({form})", flush=True)
+    # search passes (the searches' pass counts, worst cases first)
+    its = np.array([x[0] for x in iters])
+    print(f"passes per instance: mean {its.mean():.1f}, p50 {np.percentile(its, 50):.0f}, "
+          f"p99 {np.percentile(its, 99):.0f}, max {its.max()}", flush=True)
+    for x in sorted(iters, reverse=True)[:5]:
+        print(f"  {x[0]} passes: seed {x[1]} N={x[2]} T={x[3]} G={x[4]} k={x[5]:g}", flush=True)
     s.close()
 
 
