@@ -253,33 +253,56 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
  * selects), and each pick takes the first set bit (lowest, or highest) of
  * the first non-empty word; c is summed in selection order from 0.0, as the
  * twin does.  Other cases: sw_p2x_cost. */
-template <bool LO>
-static __device__ __forceinline__ double p2x_cost_dir(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
-                                                      int q, int t, int u, const double* c) {
-    if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, ws, q, t, u, c);
-    uint64_t y[4];
+template <bool LO, int NW>
+static __device__ __forceinline__ double p2x_cost_nw(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
+                                                     int q, int t, int u, const double* c) {
+    /* NW words of code for nw ≤ NW actual words (NW = 4 serves nw = 3 with
+     * a zero word): y[s] is the s-th word in scan order */
+    uint64_t y[NW];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NW; ++s) {
         const int i = LO ? s : nw - 1 - s;
         y[s] = s < nw ? (Bt[i * ws] & ~Bu[i * ws]) : 0ull;
     }
-    const int avail = __popcll(y[0]) + __popcll(y[1]) + __popcll(y[2]) + __popcll(y[3]);
+    int avail = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) avail += __popcll(y[s]);
     if (avail < q) return SW_P2X_NONE;
     double sum = 0.0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         if (g >= q) break;
-        const int s = y[0] ? 0 : y[1] ? 1 : y[2] ? 2 : 3;
-        const uint64_t ys = s == 0 ? y[0] : s == 1 ? y[1] : s == 2 ? y[2] : y[3];
+        /* the first non-empty word in scan order */
+        int sidx = NW - 1;
+        uint64_t ys = y[NW - 1];
+#pragma unroll
+        for (int s2 = NW - 2; s2 >= 0; --s2) {
+            sidx = y[s2] ? s2 : sidx;
+            ys = y[s2] ? y[s2] : ys;
+        }
         const int b = LO ? __builtin_ctzll(ys) : 63 - __builtin_clzll(ys);
         const uint64_t cl = LO ? (ys & (ys - 1)) : (ys & ~(1ull << (b & 63)));
-        y[0] = s == 0 ? cl : y[0];
-        y[1] = s == 1 ? cl : y[1];
-        y[2] = s == 2 ? cl : y[2];
-        y[3] = s == 3 ? cl : y[3];
-        sum = sum + c[64 * (LO ? s : nw - 1 - s) + (b & 63)];
+#pragma unroll
+        for (int s2 = 0; s2 < NW; ++s2) y[s2] = s2 == sidx ? cl : y[s2];
+        sum = sum + c[64 * (LO ? sidx : nw - 1 - sidx) + (b & 63)];
     }
     return sum * (double)(u - t);
+}
+
+/* sw_p2x_cost (sw_p2x.h) for classes of at most 256 jobs (≤ 4 words) and
+ * q ≤ 4, for one direction (LO: u < t, ascending ranks; else descending),
+ * specialised on the word count nw (1, 2, or up to 4; uniform per class, like
+ * q): the and-not
+ * words are loaded in scan order, each pick takes the first set bit (lowest,
+ * or highest) of the first non-empty word, and c is summed in selection order
+ * from 0.0, as the twin does.  Other cases: sw_p2x_cost. */
+template <bool LO>
+static __device__ __forceinline__ double p2x_cost_dir(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws,
+                                                      int q, int t, int u, const double* c) {
+    if (q > 4 || nw > 4) return sw_p2x_cost(Bt, Bu, nw, ws, q, t, u, c);
+    if (nw == 1) return p2x_cost_nw<LO, 1>(Bt, Bu, nw, ws, q, t, u, c);
+    if (nw == 2) return p2x_cost_nw<LO, 2>(Bt, Bu, nw, ws, q, t, u, c);
+    return p2x_cost_nw<LO, 4>(Bt, Bu, nw, ws, q, t, u, c);
 }
 
 /* W entries for load size F: every entry (all = true) or those in a row or

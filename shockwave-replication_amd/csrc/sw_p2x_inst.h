@@ -24,6 +24,13 @@
  * L2-resident while the instance runs) so that the LDS holds only the step's
  * own state (~30 KB at 900 jobs × 30 rounds).
  */
+/* thread tid's jobs [j0, j1) of an N-job instance (the plan kernel's split) */
+__device__ __forceinline__ int j0r(int N) { return (int)threadIdx.x * ((N + SW_BLOCK - 1) / SW_BLOCK); }
+__device__ __forceinline__ int j1r(int N) {
+    const int q = (N + SW_BLOCK - 1) / SW_BLOCK;
+    return min((int)threadIdx.x * q + q, N);
+}
+
 __device__ __forceinline__ void sw_p2x_instance(const sw_batch_dev& B, unsigned char* ws,
                                                 unsigned char* smem, int inst) {
     const sw_inst_dev* I = &B.inst[inst];
@@ -72,18 +79,28 @@ __device__ __forceinline__ void sw_p2x_instance(const sw_batch_dev& B, unsigned 
     const int nc = sw_p2x_block<SW_WAVES>(blk, L, var, X, A, T, G, sp);
     if (nc == 0) return;
     /* rewrite the moved jobs' plan bytes; the P2 objective of the final
-     * masks, summed like the plan kernel's emit */
+     * masks, summed like the plan kernel's emit.  The compaction offsets are
+     * counted again (one scan; B.masks is unchanged until this loop) rather
+     * than kept live through the step, where the 64-VGPR kernel spilled them */
+    /* N read again through a volatile load, so the compiler recomputes the
+     * job range and its addresses here instead of keeping the first ones */
+    const int N2 = *(volatile const int*)&I->N;
+    const int64_t jo2 = *(volatile const int64_t*)&I->job_off;
+    int act2 = 0;
+    for (int j = j0r(N2); j < j1r(N2); ++j) act2 += B.masks[jo2 + j] != 0ull;
+    int A2;
+    const int a0r = blk.exscan(act2, A2);
     uint8_t* plan = B.plan + I->plan_off;
     double acc = 0.0;
-    for (int j = j0, a = a0; j < j1; ++j) {
-        const uint64_t m0 = B.masks[jo + j];
+    for (int j = j0r(N2), a = a0r; j < j1r(N2); ++j) {
+        const uint64_t m0 = B.masks[jo2 + j];
         if (!m0) {
             acc = acc + 0.0;
             continue;
         }
         const uint64_t m = X.cm[a++];
         if (m != m0) {
-            B.masks[jo + j] = m;
+            B.masks[jo2 + j] = m;
             for (int t = 0; t < T; ++t) plan[(size_t)j * T + t] = (uint8_t)((m >> t) & 1ull);
         }
         const int cnt = __popcll(m);
@@ -93,7 +110,7 @@ __device__ __forceinline__ void sw_p2x_instance(const sw_batch_dev& B, unsigned 
                              8 * (int64_t)__popcll(m & 0xFF00FF00FF00FF00ull) +
                              16 * (int64_t)__popcll(m & 0xFFFF0000FFFF0000ull) +
                              32 * (int64_t)__popcll(m & 0xFFFFFFFF00000000ull);
-        acc = acc + ((double)Ssum / (double)cnt) * B.p[jo + j];
+        acc = acc + ((double)Ssum / (double)cnt) * B.p[jo2 + j];
     }
     const double P2 = blk.detsum(acc);
     if (threadIdx.x == 0) {
