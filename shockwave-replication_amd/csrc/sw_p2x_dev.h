@@ -147,6 +147,9 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
         __syncthreads();
         BF_STAMP(9);
         if (wv == 0) {
+            /* the sweep's serial part: the other waves wait at the barrier,
+             * so issue it ahead of the CU's other workgroups */
+            __builtin_amdgcn_s_setprio(3);
             double d = act ? L->bd[lane] : 0.0;
             int pr = act ? L->bp[lane] : -1;
             const double dV = L->bd[T];
@@ -238,6 +241,7 @@ static __device__ __forceinline__ void p2x_find_cycle(sw_p2x_lds* L, const doubl
                 if (!done && it == T && lane == 0) L->len = 0;
             }
             if (lane == 0) L->bfdone = done;
+            __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();
         if (L->bfdone) break;

@@ -403,7 +403,11 @@ __device__ __forceinline__ void sw_pack_rounds_wave_io(sw_pack_lds* L, int T, in
     uint32_t st[E1];
 #pragma unroll
     for (int i = 0; i < E1; ++i) st[i] = xst[E1 * lane + i];
+    /* the loop is the instance's critical path while the CU's other
+     * workgroups run phases that only need throughput: issue it first */
+    __builtin_amdgcn_s_setprio(3);
     sw_pack_rounds_wave<E1>(L, T, G, st, xmk, caps, swp);
+    __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int i = 0; i < E1; ++i) xst[E1 * lane + i] = st[i];
 }
