@@ -266,6 +266,16 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
     const int lane = lane_id();
     SWP_DECL;
     int32_t* Hm = L->Hc[lane & 7]; /* this lane's histogram copy */
+    /* the state carries, besides the rounds still to place (rr) and the
+     * width, the rounds still to place of a position not yet taken this
+     * round (ra, 0 once taken): every eligibility test is one compare of ra */
+    /* st[i] here: rr | w << 8 | ra << 16, one byte each (the compares read
+     * the bytes in place) */
+#define RR_(i) ((int32_t)(st[i] & 0xFFu))
+#define WW_(i) ((int32_t)((st[i] >> 8) & 0xFFu))
+#define RA_(i) ((int32_t)((st[i] >> 16) & 0xFFu))
+#pragma unroll
+    for (int i = 0; i < E1; ++i) st[i] = (st[i] & 0xFFFFu) | ((st[i] & 0xFFu) << 16);
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         L->Hc[c][lane] = 0;
@@ -276,7 +286,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
     wave_sync();
 #pragma unroll
     for (int i = 0; i < E1; ++i)
-        if (st[i] != 0u) atomicAdd(&Hm[pk_r(st[i])], (int32_t)pk_w(st[i]));
+        if (st[i] != 0u) atomicAdd(&Hm[RR_(i)], WW_(i));
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
@@ -315,18 +325,17 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
 #pragma unroll
             for (int i = 0; i < E1; ++i) {
                 pre[i] = lt;
-                lt += (!pk_sel(st[i]) && (int)pk_r(st[i]) > m) ? (int32_t)pk_w(st[i]) : 0;
+                lt += RA_(i) > m ? WW_(i) : 0;
             }
             const int32_t base = wave_incscan_i32(lt) - lt;
             SWP_STAMP(7);
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E1; ++i) {
-                const int32_t w = (int32_t)pk_w(st[i]);
                 const int32_t ex = base + pre[i];
-                const bool take = !pk_sel(st[i]) && (int)pk_r(st[i]) > m && ex < q && ex + w <= cap;
-                st[i] |= take ? (1u << 16) : 0u;
-                took += take ? w : 0;
+                const bool take = RA_(i) > m && ex < q && ex + WW_(i) <= cap;
+                took += take ? WW_(i) : 0;
+                st[i] = take ? (st[i] & 0xFFFFu) : st[i];
             }
             took = wave_sum_i32(took);
             cap -= took;
@@ -341,16 +350,15 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
 #pragma unroll
             for (int i = 0; i < E1; ++i) {
                 pre[i] = lt;
-                lt += (!pk_sel(st[i]) && pk_r(st[i]) > 0) ? (int32_t)pk_w(st[i]) : 0;
+                lt += RA_(i) > 0 ? WW_(i) : 0;
             }
             const int32_t base = wave_incscan_i32(lt) - lt;
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E1; ++i) {
-                const int32_t w = (int32_t)pk_w(st[i]);
-                const bool take = !pk_sel(st[i]) && pk_r(st[i]) > 0 && base + pre[i] + w <= cap;
-                st[i] |= take ? (1u << 16) : 0u;
-                took += take ? w : 0;
+                const bool take = RA_(i) > 0 && base + pre[i] + WW_(i) <= cap;
+                took += take ? WW_(i) : 0;
+                st[i] = take ? (st[i] & 0xFFFFu) : st[i];
             }
             cap -= wave_sum_i32(took);
         }
@@ -359,31 +367,37 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
             int32_t best = 0x7FFFFFFF;
 #pragma unroll
             for (int i = E1 - 1; i >= 0; --i) {
-                const bool ok = !pk_sel(st[i]) && pk_r(st[i]) > 0 && (int32_t)pk_w(st[i]) <= cap;
-                best = ok ? (((E1 * lane + i) << 8) | (int32_t)pk_w(st[i])) : best;
+                const bool ok = RA_(i) > 0 && WW_(i) <= cap;
+                best = ok ? (((E1 * lane + i) << 8) | WW_(i)) : best;
             }
             best = wave_min_i32(best);
             SWP_COUNT(19);
             if (best == 0x7FFFFFFF) break;
             const int pos = best >> 8;
 #pragma unroll
-            for (int i = 0; i < E1; ++i) st[i] |= (E1 * lane + i == pos) ? (1u << 16) : 0u;
+            for (int i = 0; i < E1; ++i) st[i] = (E1 * lane + i == pos) ? (st[i] & 0xFFFFu) : st[i];
             cap -= best & 0xFF;
         }
         SWP_STAMP(4);
 #pragma unroll
         for (int i = 0; i < E1; ++i) {
-            const bool sel = pk_sel(st[i]) != 0;
-            const uint32_t r = pk_r(st[i]);
-            st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
+            const int32_t r = RR_(i);
+            const bool sel = RA_(i) == 0 && r > 0;
             if (sel) {
-                atomicAdd(&Hm[r], -(int32_t)pk_w(st[i]));
-                atomicAdd(&Hm[r - 1], (int32_t)pk_w(st[i]));
+                atomicAdd(&Hm[r], -WW_(i));
+                atomicAdd(&Hm[r - 1], WW_(i));
                 atomicOr((unsigned long long*)&xmk[E1 * lane + i], 1ull << t);
             }
+            const uint32_t r2 = (uint32_t)(r - (sel ? 1 : 0));
+            st[i] = r2 | (st[i] & 0xFF00u) | (r2 << 16);
         }
         SWP_STAMP(5);
     }
+#pragma unroll
+    for (int i = 0; i < E1; ++i) st[i] &= 0xFFFFu;
+#undef RR_
+#undef WW_
+#undef RA_
     SWP_FLUSH;
     wave_sync();
 }
