@@ -51,3 +51,24 @@ def test_gpu_fuzz_onchip_batch_paths_match_twin(count, gpu_solver, twin):
     for i, (a, r) in enumerate(zip(probs, rb)):
         check_plan_valid(a, r)
         assert_same_result(r, twin.solve(a), f"{count}-batch case {i} N={a.N} G={a.G} T={a.T}")
+
+
+def test_gpu_split_pack_loop_widths_match_twin(gpu_solver, twin):
+    """The split path's pack kernel runs its one-wave round loop with 2, 4, 6
+    or 8 positions per lane by the instance's active-job count A
+    (csrc/sw_pack.h sw_pack_rounds_one); one 1,100-instance batch of C3-shaped
+    instances whose sizes put A in every one of those ranges (and above 512,
+    where the slow-path kernel takes over), each instance bit-identical with
+    the twin."""
+    import sw_synth as ss
+    sizes = [(60, 32), (150, 64), (300, 96), (420, 128), (600, 160), (900, 256), (1024, 384),
+             (1024, 512)]
+    probs = [ss.synth_problem(7000 + i, *sizes[i % len(sizes)]) for i in range(1100)]
+    rb = gpu_solver.solve_batch(probs)
+    ranges = set()
+    for i, (a, r) in enumerate(zip(probs, rb)):
+        check_plan_valid(a, r)
+        assert_same_result(r, twin.solve(a), f"case {i} N={a.N} G={a.G}")
+        act = int((r["planned_rounds"] > 0).sum())
+        ranges.add(0 if act <= 128 else 1 if act <= 256 else 2 if act <= 384 else 3 if act <= 512 else 4)
+    assert {0, 1, 2, 3, 4} <= ranges, ranges  # 4: more than 512, the slow-path kernel
