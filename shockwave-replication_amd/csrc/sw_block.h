@@ -364,9 +364,9 @@ struct sw_blk_t {
             b = X->u2[par][k][1] < b ? X->u2[par][k][1] : b;
         }
         flip();
-        S = sw_i64(t);
-        MX = sw_u64(a);
-        MN = sw_u64(b);
+        S = t;
+        MX = a;
+        MN = b;
     }
 
     /* Σ v, max mx and min mn of non-negative 32-bit values, one barrier
