@@ -436,8 +436,10 @@ __device__ __forceinline__ void sw_pack_rounds_one(sw_pack_lds* L, int A, int T,
     xst[threadIdx.x] = st1; /* 0 past A */
     __syncthreads();
     if (wave_id() == 0) {
-        if (!MULTI) sw_pack_rounds_wave_io<8>(L, T, G, xst, xmk, caps, swp);
-        else if (A <= 128) sw_pack_rounds_wave_io<2>(L, T, G, xst, xmk, caps, swp);
+        if (!MULTI) {
+            if (A <= 384) sw_pack_rounds_wave_io<6>(L, T, G, xst, xmk, caps, swp);
+            else sw_pack_rounds_wave_io<8>(L, T, G, xst, xmk, caps, swp);
+        } else if (A <= 128) sw_pack_rounds_wave_io<2>(L, T, G, xst, xmk, caps, swp);
         else if (A <= 256) sw_pack_rounds_wave_io<4>(L, T, G, xst, xmk, caps, swp);
         else if (A <= 384) sw_pack_rounds_wave_io<6>(L, T, G, xst, xmk, caps, swp);
         else sw_pack_rounds_wave_io<8>(L, T, G, xst, xmk, caps, swp);
