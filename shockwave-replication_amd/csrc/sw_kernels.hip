@@ -1129,8 +1129,8 @@ struct Ctx {
                 uint64_t mk1[1] = {0ull};
                 /* the round loop in wave 0 (sw_pack_rounds_one; the sort is
                  * done with sbuf, whose first 6 KB stage the states): the
-                 * pack kernel sizes it by A, the plan kernel takes the
-                 * 8-position form only (its register file has no room for
+                 * pack kernel sizes it by A, the plan kernel takes the 6-
+                 * or 8-position form (its register file has no room for
                  * four copies) */
 #ifdef SW_STAMPS
                 sw_pack_rounds_one<SMALL>(PL, A_, T, G, st1[0], mk1[0], sbuf, capsp, swp);

@@ -407,7 +407,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
  * call) into wave 0, which runs sw_pack_rounds_wave<E1> with E1 the even
  * number of positions per lane that covers A (2, 4, 6 or 8: a runtime bound
  * inside the unrolled loops costs the kernel's register budget) when MULTI,
- * else always 8 (the plan kernel, whose register file the extra copies would
+ * else 6 or 8 (the plan kernel, whose register file four copies would
  * overflow); every thread of the block must call it. */
 template <int E1>
 __device__ __forceinline__ void sw_pack_rounds_wave_io(sw_pack_lds* L, int T, int G, uint32_t* xst,
