@@ -70,13 +70,17 @@ __device__ __forceinline__ uint32_t pk_sel(uint32_t s) { return (s >> 16) & 1u; 
 
 /* LDS the round loop needs: the running histogram Hu (H[0]); the rest is
  * spare (kept for the carve-up of sw_kernels.hip). */
+#ifndef SW_HCOPIES
+#define SW_HCOPIES 4
+#endif
 struct sw_pack_lds {
     int32_t H[2][68];
     int32_t SH[2][68];
-    /* the one-wave loop's histogram, in 8 copies by lane & 7: the positions a
-     * round places mostly share one or two remaining-round counts, and their
-     * atomics on one bin serialised in the LDS (copy c's bin v sits in bank
-     * 8c + v, so the copies of a bin never share a bank) */
+    /* the one-wave loop's histogram, in SW_HCOPIES copies by lane: the
+     * positions a round places mostly share one or two remaining-round counts,
+     * and their atomics on one bin serialise in the LDS (copy c's bin v sits
+     * in bank 8c + v, so the copies of a bin never share a bank); four copies
+     * measured best against one, two and eight (each round sums them) */
     int32_t Hc[8][72];
 };
 
@@ -252,7 +256,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
  * eight waves and waits at two barriers per tier; here one wave issues each
  * step once and never waits for the others (on a C3 instance the round loop
  * was two thirds of the pack kernel's VALU instructions).  The histogram
- * (L->Hc, eight copies summed at each round's start) is updated by this wave
+ * (L->Hc, four copies summed at each round's start) is updated by this wave
  * alone, so its LDS atomics and reads stay in program order.
  * Called by wave 0 only; st as in sw_pack_rounds, the round masks go to
  * xmk[position] (LDS or workspace) with an atomic OR per placement instead
@@ -265,7 +269,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
     (void)swp;
     const int lane = lane_id();
     SWP_DECL;
-    int32_t* Hm = L->Hc[lane & 7]; /* this lane's histogram copy */
+    int32_t* Hm = L->Hc[lane & (SW_HCOPIES - 1)]; /* this lane's histogram copy */
     /* the state carries, besides the rounds still to place (rr) and the
      * width, the rounds still to place of a position not yet taken this
      * round (ra, 0 once taken): every eligibility test is one compare of ra */
@@ -277,7 +281,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
 #pragma unroll
     for (int i = 0; i < E1; ++i) st[i] = (st[i] & 0xFFFFu) | ((st[i] & 0xFFu) << 16);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < SW_HCOPIES; ++c) {
         L->Hc[c][lane] = 0;
         if (lane < 8) L->Hc[c][64 + lane] = 0;
     }
@@ -296,7 +300,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
         wave_sync(); /* the copies hold the placements of round t − 1 */
         int32_t h0 = 0, h1 = 0; /* bins lane and lane + 1, the copies summed */
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
+        for (int c = 0; c < SW_HCOPIES; ++c) {
             h0 += L->Hc[c][lane];
             h1 += L->Hc[c][lane + 1];
         }
