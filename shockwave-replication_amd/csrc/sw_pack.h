@@ -81,7 +81,7 @@ struct sw_pack_lds {
      * and their atomics on one bin serialise in the LDS (copy c's bin v sits
      * in bank 8c + v, so the copies of a bin never share a bank); four copies
      * measured best against one, two and eight (each round sums them) */
-    int32_t Hc[8][72];
+    int32_t Hc[SW_HCOPIES][72];
 };
 
 /*
