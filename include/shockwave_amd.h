@@ -65,6 +65,12 @@ extern "C" {
 /* The exchange step (negative-cycle cancelling over round moves, DESIGN.md
  * §3.6) improved the kept P2 placement. */
 #define SW_STATUS_P2_EXCHANGED 0x40
+/* The P1 objective is not certified within 1e-3 of `bound` (an upper bound
+ * on the reference MILP's P1 optimum): bound − objective > 1e-3·|objective|.
+ * Set where fragmenting widths or a lumpy level structure leave the greedy
+ * rounding short of the relaxation, so a caller can tell a certified plan
+ * from a best effort. */
+#define SW_STATUS_P1_UNCERTIFIED 0x80
 
 /*
  * One plan solve.  Field ↔ reference:
@@ -108,7 +114,9 @@ typedef struct sw_problem {
  *   utility       the first term alone
  *   makespan      max_j max(0, R_j − d_j·e_j)                              shockwave.py:260-263, :363
  *   p2_objective  Σ_{n_j>0} p_j·(Σ_t t·y_jt)/n_j                           shockwave.py:309-322
- *   bound         an upper bound on the aggregate P1 optimum (fractional-knapsack bound)
+ *   bound         an upper bound on the aggregate P1 optimum (and so on the
+ *                 reference MILP's): the largest Lagrangian bound the level
+ *                 search's branch and bound leaves (sw_bnb.h)
  *   iters         number of level/price evaluations the solver made
  * plan_masks (optional, ABI 2) is the same plan bit-packed: one word per job,
  * bit t = plan[j][t] — 8 bytes per job across the host boundary instead of

@@ -29,6 +29,7 @@
 
 #include "../include/shockwave_amd.h"
 #include "../shockwave-replication_amd/csrc/sw_arith.h"
+#include "../shockwave-replication_amd/csrc/sw_bnb.h"
 #include "../shockwave-replication_amd/csrc/sw_repair.h"
 #include "../shockwave-replication_amd/csrc/sw_reround.h"
 #include "../shockwave-replication_amd/csrc/sw_validate.h"
@@ -357,6 +358,9 @@ static void pack(const twin_t* P, const int32_t* nin, const uint64_t* k1, const 
  * repacks every changed class alone (unit widths, order p_j/n_j) inside its
  * new capacities; unchanged classes keep their density rows.  Writes yout
  * and placed; returns 1 when every round of nin is placed. */
+static int repack_classes(const twin_t* P, const sw_problem* pr, const int32_t* nin,
+                          const sw_repair_t* Rp, uint8_t* yout, int32_t* placed);
+
 static int repair_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin, const uint8_t* yd,
                        const int32_t* pd, uint8_t* yout, int32_t* placed) {
     const int32_t N = P->N, T = P->T;
@@ -377,6 +381,17 @@ static int repair_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin
     size_t NN = N > 0 ? (size_t)N : 1;
     memcpy(yout, yd, NN * (size_t)T);
     memcpy(placed, pd, sizeof(int32_t) * NN);
+    return repack_classes(P, pr, nin, &R, yout, placed);
+}
+
+/* Repack every changed class of the profile R alone with unit widths, order
+ * p_j/n_j, inside its per-round capacities R->caps; the other rows of yout /
+ * placed are kept.  Returns 1 when every round of nin is placed. */
+static int repack_classes(const twin_t* P, const sw_problem* pr, const int32_t* nin,
+                          const sw_repair_t* Rp, uint8_t* yout, int32_t* placed) {
+    const int32_t N = P->N, T = P->T;
+    const sw_repair_t R = *Rp;
+    size_t NN = N > 0 ? (size_t)N : 1;
     int32_t* nc = (int32_t*)malloc(sizeof(int32_t) * NN);
     int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * NN);
     uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
@@ -400,6 +415,41 @@ static int repair_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin
     for (int32_t j = 0; j < N; ++j) ok &= (placed[j] == nin[j]);
     free(nc); free(pc); free(k1); free(k2); free(yc);
     return ok;
+}
+
+/* Pattern placement (sw_profile_search): when neither the density order nor
+ * its repair places nin, search an exact width-class profile over round
+ * patterns and pack every class inside it (unit widths, order p_j/n_j).
+ * Writes yout and placed; returns 1 when every round of nin is placed. */
+static int pattern_pack(const twin_t* P, const sw_problem* pr, const int32_t* nin, uint8_t* yout,
+                        int32_t* placed) {
+    const int32_t N = P->N, T = P->T;
+    sw_repair_t R;
+    memset(&R, 0, sizeof(R));
+    int32_t A = 0;
+    for (int32_t j = 0; j < N; ++j)
+        if (nin[j] > 0) {
+            if (sw_repair_add_class(&R, P->jc[j].w) < 0) return 0;
+            ++A;
+        }
+    if (A == 0) return 0;
+    int32_t* hist = (int32_t*)calloc((size_t)R.ncls * (T + 1), sizeof(int32_t));
+    int32_t* scratch = (int32_t*)malloc(sizeof(int32_t) * (size_t)SW_PAT_SCRATCH(A));
+    for (int32_t j = 0; j < N; ++j)
+        if (nin[j] > 0) {
+            const int32_t c = sw_repair_class(&R, P->jc[j].w);
+            R.M[c] += 1;
+            hist[c * (T + 1) + nin[j]] += 1;
+        }
+    int64_t nodes = 0;
+    const int32_t found = sw_profile_search(&R, T, P->G, hist, scratch, &nodes);
+    free(hist);
+    free(scratch);
+    if (!found) return 0;
+    size_t NN = N > 0 ? (size_t)N : 1;
+    memset(yout, 0, NN * (size_t)T);
+    for (int32_t j = 0; j < N; ++j) placed[j] = 0;
+    return repack_classes(P, pr, nin, &R, yout, placed);
 }
 
 /* The packer over plain arrays, for the sharded CPU engine (oracle/shard_twin.c):
@@ -528,43 +578,38 @@ static double level_search(twin_t* P, int32_t* n, int32_t* nb, int32_t* l, int32
     if (ev.J > best.J || (ev.J == best.J && ev.Mact < best.Mact)) {
         best = ev; memcpy(nb, n, sizeof(int32_t) * NN);
     }
-    const uint32_t rho_inf = ev.rho; /* ρ*(+∞): a lower bound at every level */
-    const double U_inf = ev.U, M_free = ev.Mact, ubound_inf = ev.ubound;
-    /* golden-section search on [a, b] that reuses the surviving interior
-     * point (one new level per shrink); every probe's price is bracketed
-     * by its evaluated neighbours (a and the other interior point, or b) */
-    double width = (U_inf - elo.U) / P->k;
-    double a = M_lo, b = sw_min(M_free, M_lo + width);
-    uint32_t ra = elo.rho, rb = rho_inf; /* ρ*(a); a lower bound of ρ*(b) */
-    if (a < b && levels_between(P, a, b) > 0) {
-        double m1 = a + (b - a) * SW_GS_A;
-        double m2 = a + (b - a) * SW_GS_B;
-        sel_eval_t e1, e2;
-        select_level(P, m1, 0, n, l, tk, tmp, &e1, rb, ra);
-        if (e1.J > best.J || (e1.J == best.J && e1.Mact < best.Mact)) {
-            best = e1; memcpy(nb, n, sizeof(int32_t) * NN);
+    /* Branch and bound over the levels in (M_lo, M_free] (sw_bnb.h): plans
+     * with makespan M_lo or ≥ M_free are bounded by the two evaluated
+     * points; an open interval (a, b] by Vub(b) − k·a.  The interval of
+     * largest bound is split at its midpoint; ρ*(b) ≤ ρ*(m) ≤ ρ*(a) brackets
+     * the probe's price. */
+    const double kk = P->k, M_free = ev.Mact;
+    double cert = sw_max(elo.ubound - kk * M_lo, ev.ubound - kk * M_free);
+    sw_bnb_ivl L[SW_BNB_CAP];
+    int32_t nL = 0, probes = 0;
+    if (M_lo < M_free) L[nL++] = sw_bnb_make(M_lo, M_free, ev.ubound, elo.rho, ev.rho);
+    while (nL > 0) {
+        double kb;
+        const int32_t i = sw_bnb_pick(L, nL, kk, &kb);
+        if (kb <= best.J) break; /* nothing left can beat the best plan */
+        if (probes == SW_BNB_PROBES) { cert = sw_max(cert, kb); break; }
+        const sw_bnb_ivl I = L[i];
+        L[i] = L[--nL];
+        if (levels_between(P, I.a, I.b) == 0) { /* only b itself, if b is a level */
+            cert = sw_max(cert, I.vb - kk * I.b);
+            continue;
         }
-        select_level(P, m2, 0, n, l, tk, tmp, &e2, rb, e1.rho);
-        if (e2.J > best.J || (e2.J == best.J && e2.Mact < best.Mact)) {
-            best = e2; memcpy(nb, n, sizeof(int32_t) * NN);
+        const double m = sw_bnb_mid(I.a, I.b);
+        sel_eval_t e;
+        select_level(P, m, 0, n, l, tk, tmp, &e, I.rb, I.ra);
+        ++probes;
+        if (e.J > best.J || (e.J == best.J && e.Mact < best.Mact)) {
+            best = e; memcpy(nb, n, sizeof(int32_t) * NN);
         }
-        for (int it = 0; it < SW_GS_ITERS; ++it) {
-            const int left = e1.J >= e2.J;
-            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
-            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
-            if (!(a < b)) break;
-            if (levels_between(P, a, b) == 0) break;
-            sel_eval_t* e = left ? &e1 : &e2;
-            double m;
-            if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
-            else { m2 = a + (b - a) * SW_GS_B; m = m2; }
-            select_level(P, m, 0, n, l, tk, tmp, e, left ? e2.rho : rb, left ? ra : e1.rho);
-            if (e->J > best.J || (e->J == best.J && e->Mact < best.Mact)) {
-                best = *e; memcpy(nb, n, sizeof(int32_t) * NN);
-            }
-        }
+        if (sw_bnb_key(e.ubound, kk, I.a) > best.J) L[nL++] = sw_bnb_make(I.a, m, e.ubound, I.ra, e.rho);
+        if (sw_bnb_key(I.vb, kk, m) > best.J) L[nL++] = sw_bnb_make(m, I.b, I.vb, e.rho, I.rb);
     }
-    return ubound_inf - P->k * M_lo;
+    return sw_max(cert, best.J);
 }
 
 /* Fill of stranded capacity (the reference MILP packs per
@@ -899,6 +944,20 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
                     P.passes++;
                 }
                 if (dfc == 0) { Jp = Jo; dens = 1; break; }
+                /* neither places nb: an exact width-class profile over round
+                 * patterns, when one exists (sw_profile_search) — the counts
+                 * are P1's as they are, no re-solve; P2 then starts from (b) */
+                if (pattern_pack(&P, pr, nb, y1, placed)) {
+                    Mp = 0.0;
+                    for (int32_t j = 0; j < N; ++j) {
+                        tmp[j] = fval(&P, j, placed[j]);
+                        Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
+                    }
+                    Jp = sw_detsum(tmp, N) - P.k * Mp;
+                    P.passes++;
+                    deficit = 0;
+                    break;
+                }
                 continue;
             }
             if (ord == 0 || Jo > Jp) {
@@ -1045,6 +1104,7 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     res->makespan = Mact;
     res->objective = U - P.k * Mact;
     res->bound = bound;
+    if (sw_p1_uncertified(res->objective, bound)) status |= SW_STATUS_P1_UNCERTIFIED;
     res->iters = (int32_t)P.passes;
     res->status = status;
     if (res->plan && N > 0) memcpy(res->plan, yf, (size_t)N * T);

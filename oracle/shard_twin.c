@@ -406,7 +406,9 @@ static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_
         if (E->arr[src][i] <= 0) continue;
         const int32_t w = E->jc[i].w;
         if (w == wc) {
-            for (int32_t t = 0; t < E->T; ++t) buf[t] += (int64_t)((E->y[ysrc][i] >> t) & 1u);
+            if (psrc == SW_CLASS_HIST) buf[E->arr[src][i] - 1] += 1; /* count histogram */
+            else
+                for (int32_t t = 0; t < E->T; ++t) buf[t] += (int64_t)((E->y[ysrc][i] >> t) & 1u);
             buf[E->T] += 1;
             if (psrc >= 0) buf[E->T + 1] += E->arr[src][i] - E->arr[psrc][i];
         }

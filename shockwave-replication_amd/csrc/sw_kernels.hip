@@ -34,6 +34,7 @@
 #include "sw_block.h"
 #include "sw_device.h"
 #include "sw_pack.h"
+#include "sw_bnb.h"
 #include "sw_repair.h"
 #include "sw_reround_dev.h"
 #include "sw_p2x_inst.h"
@@ -180,6 +181,7 @@ struct Ctx {
     int32_t* caps;
     int64_t* misc;
     sw_repair_t* rep; /* LDS: the width profile of repair_pack */
+    sw_bnb_ivl* bnb;  /* the level search's interval list (SW_BNB_CAP entries, sw_bnb.h) */
     /* this thread's jobs (ONE): slot s ↔ job jlo() + s */
     sw_job_lds JL; /* ONE: per-job constants, SoA in LDS (not VGPRs) */
     float kr[SW_JPT][KT];
@@ -673,24 +675,20 @@ struct Ctx {
 
     /* twin: level_search — best counts land in nbest; returns the bound.
      * Written as a loop over evaluation requests so select_level has a
-     * single call site (phase 1: M = M_lo; 0: M = +inf; 2 / 3: the first
-     * golden pair m1, m2; 4 / 5: the new m1 / m2 after a shrink that kept
-     * the other point). */
+     * single call site (phase 1: M = M_lo; 0: M = +inf; 2: a branch-and-
+     * bound probe at the midpoint of the interval of largest bound). */
     __device__ __forceinline__ double level_search() {
 #ifdef SW_STAMPS
         ls_t = __builtin_amdgcn_s_memtime();
         for (int k = 0; k < 9; ++k) lsa[k] = 0;
 #endif
-        SelEval best, e1, e2, elo;
+        SelEval best, elo;
         best.U = best.Mact = best.ubound = 0.0;
         best.J = -1e308;
         best.rho = 0;
-        e1 = best;
-        e2 = best;
         elo = best;
         double M_lo = 0.0, ret = 0.0;
-        double a = 0.0, b = 0.0, m1 = 0.0, m2 = 0.0;
-        uint32_t rb = 0, ra = 0, plo = 0, phi = SW_KEY_INF_BITS;
+        uint32_t plo = 0, phi = SW_KEY_INF_BITS;
         const bool levels = N > 0 && k > 0.0;
         if (levels) {
             /* twin: the M_lo search on [lb, top] that snaps to row values */
@@ -738,12 +736,18 @@ struct Ctx {
             M_lo = sw_uni(sw_from_bits(lo));
             LS_STAMP(5);
         }
-        int phase = levels ? 1 : 0, it = 0;
+        int phase = levels ? 1 : 0;
+        /* branch and bound over the levels in (M_lo, M_free] (twin:
+         * level_search; sw_bnb.h): the interval list lives in bnb, written
+         * by thread 0 between barriers; every thread picks from it alike */
+        int32_t nL = 0, probes = 0;
+        double cert = 0.0, m = 0.0;
+        double Ia = 0.0, Ib = 0.0, Ivb = 0.0;
+        uint32_t Ira = 0, Irb = 0;
         while (true) {
             double M = 0.0;
             if (phase == 1) M = M_lo;
-            else if (phase == 2 || phase == 4) M = m1;
-            else if (phase >= 3) M = m2;
+            else if (phase == 2) M = m;
             const SelEval ev = sw_uni(select_level(M, phase == 0, plo, phi));
             if (phase == 1) {
                 best = ev;
@@ -772,50 +776,58 @@ struct Ctx {
                     break;
                 }
                 keep_best(ev, best);
-                ret = sw_uni(ev.ubound - k * M_lo);
-                const double width = (ev.U - elo.U) / k;
-                a = M_lo;
-                b = sw_uni(sw_min(ev.Mact, M_lo + width));
-                ra = elo.rho;
-                rb = ev.rho;
-                it = 0;
-                if (!(a < b)) break;
-                if (levels_between(a, b) == 0) break;
-                m1 = sw_uni(a + (b - a) * SW_GS_A);
-                m2 = sw_uni(a + (b - a) * SW_GS_B);
-                plo = rb;
-                phi = ra;
-                phase = 2;
-                continue;
+                cert = sw_uni(sw_max(elo.ubound - k * M_lo, ev.ubound - k * ev.Mact));
+                if (M_lo < ev.Mact) {
+                    if (threadIdx.x == 0) bnb[0] = sw_bnb_make(M_lo, ev.Mact, ev.ubound, elo.rho, ev.rho);
+                    nL = 1;
+                }
+            } else { /* a probe at the midpoint m of the interval I */
+                keep_best(ev, best);
+                ++probes;
+                const bool pl = sw_bnb_key(ev.ubound, k, Ia) > best.J;
+                const bool pr = sw_bnb_key(Ivb, k, m) > best.J;
+                if (threadIdx.x == 0) {
+                    int32_t n2 = nL;
+                    if (pl) bnb[n2++] = sw_bnb_make(Ia, m, ev.ubound, Ira, ev.rho);
+                    if (pr) bnb[n2++] = sw_bnb_make(m, Ib, Ivb, ev.rho, Irb);
+                }
+                nL += (pl ? 1 : 0) + (pr ? 1 : 0);
             }
-            keep_best(ev, best);
-            if (phase == 2) {
-                e1 = ev;
-                plo = rb;
-                phi = e1.rho;
-                phase = 3;
-                continue;
+            /* the next interval worth a probe */
+            bool more = false;
+            while (nL > 0) {
+                __syncthreads(); /* thread 0's list writes are visible */
+                double kb;
+                const int32_t i = sw_u32(sw_bnb_pick(bnb, nL, k, &kb));
+                kb = sw_uni(kb);
+                if (kb <= best.J) break; /* nothing left can beat the best plan */
+                if (probes == SW_BNB_PROBES) {
+                    cert = sw_uni(sw_max(cert, kb));
+                    break;
+                }
+                Ia = sw_uni(bnb[i].a);
+                Ib = sw_uni(bnb[i].b);
+                Ivb = sw_uni(bnb[i].vb);
+                Ira = sw_uni(bnb[i].ra);
+                Irb = sw_uni(bnb[i].rb);
+                __syncthreads(); /* every thread has read the list */
+                if (threadIdx.x == 0) bnb[i] = bnb[nL - 1];
+                --nL;
+                if (levels_between(Ia, Ib) == 0) { /* only b itself, if b is a level */
+                    cert = sw_uni(sw_max(cert, Ivb - k * Ib));
+                    continue;
+                }
+                m = sw_uni(sw_bnb_mid(Ia, Ib));
+                plo = Irb;
+                phi = Ira;
+                more = true;
+                break;
             }
-            if (phase == 4) e1 = ev; else e2 = ev; /* phases 3, 5 */
-            /* golden-section shrink that keeps the surviving interior point */
-            if (it >= SW_GS_ITERS) break;
-            const bool left = e1.J >= e2.J;
-            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
-            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
-            ++it;
-            if (!(a < b)) break;
-            if (levels_between(a, b) == 0) break;
-            if (left) {
-                m1 = sw_uni(a + (b - a) * SW_GS_A);
-                plo = e2.rho;
-                phi = ra;
-                phase = 4;
-            } else {
-                m2 = sw_uni(a + (b - a) * SW_GS_B);
-                plo = rb;
-                phi = e1.rho;
-                phase = 5;
+            if (!more) {
+                ret = sw_uni(sw_max(cert, best.J));
+                break;
             }
+            phase = 2;
         }
         lsU = best.U;
         lsM = best.Mact;
@@ -1306,6 +1318,74 @@ struct Ctx {
         return blk.sum(bad) == 0;
     }
 
+    /*
+     * twin: pattern_pack — neither the density order nor its repair placed
+     * nin: the width classes' count histograms are gathered (LDS atomics),
+     * one thread searches an exact class profile over round patterns
+     * (sw_profile_search, scratch in scr), and every class is packed inside
+     * it (pack mode 5) into y / pout, which hold the density pack of nin.
+     * True when every round of nin is placed.
+     */
+    __device__ __forceinline__ bool pattern_pack(const uint8_t* nin, uint64_t* y, uint8_t* pout,
+                                                 int32_t* scr) {
+        sw_repair_t* R = rep;
+        uint32_t* wset = reinterpret_cast<uint32_t*>(misc); /* widths present: 256 bits */
+        int32_t* flag = reinterpret_cast<int32_t*>(misc) + 8;
+        __syncthreads(); /* earlier users of caps / misc are done */
+        for (int i = threadIdx.x; i < (int)(sizeof(sw_repair_t) / 4); i += SW_BLOCK)
+            reinterpret_cast<int32_t*>(R)[i] = 0;
+        if (threadIdx.x < 8) wset[threadIdx.x] = 0;
+        __syncthreads();
+        for_jobs([&](int j, int s) {
+            (void)s;
+            if (nin[j] > 0) atomicOr(&wset[(w_in[j] >> 5) & 7], 1u << (w_in[j] & 31));
+        });
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int32_t n = 0;
+            for (int wd = 0; wd < 8; ++wd) {
+                uint32_t msk = wset[wd];
+                while (msk) {
+                    const int b = __builtin_ctz(msk);
+                    msk &= msk - 1u;
+                    if (n < SW_RCLS_MAX) R->wc[n] = wd * 32 + b;
+                    ++n;
+                }
+            }
+            R->ncls = n;
+        }
+        __syncthreads();
+        const int K = R->ncls;
+        if (K > SW_RCLS_MAX || K == 0) return false; /* uniform */
+        const int HT = T + 1;
+        for (int i = threadIdx.x; i < K * HT; i += SW_BLOCK) scr[i] = 0;
+        __syncthreads();
+        for_jobs([&](int j, int s) {
+            (void)s;
+            if (nin[j] > 0) {
+                const int32_t c = sw_repair_class(R, w_in[j]);
+                atomicAdd(&R->M[c], 1);
+                atomicAdd(&scr[c * HT + nin[j]], 1);
+            }
+        });
+        __syncthreads();
+        if (threadIdx.x == 0) flag[0] = sw_profile_search(R, T, G, scr, scr + K * HT, nullptr);
+        __syncthreads();
+        if (flag[0] == 0) return false; /* uniform */
+        for (int ci = 0; ci < K; ++ci) {
+            __syncthreads(); /* the previous class's pack has read caps */
+            if (threadIdx.x < 64) caps[threadIdx.x] = threadIdx.x < T ? R->caps[ci][threadIdx.x] : 0;
+            pwc = R->wc[ci];
+            pack(5, nin, y, pout);
+        }
+        int64_t bad = 0;
+        for_jobs([&](int j, int s) {
+            (void)s;
+            bad += pout[j] != nin[j];
+        });
+        return blk.sum(bad) == 0;
+    }
+
     /* The round loop of pack, run by wave 0 alone (twin: the t loop of
      * pack).  Lane L owns positions [L·PPL, L·PPL + PPL) (prefix order =
      * lane-major); their state lives at tslot(p). */
@@ -1521,6 +1601,10 @@ __device__ __forceinline__ void level_instance(const sw_batch_dev& B, unsigned c
     c.tkcur = stage + 2 * NJ;
     c.nbest = stage + 3 * NJ;
     c.tiecur = stage + 4 * NJ;
+    static_assert(sizeof(float) * SW_JPT * SW_SETUP_CH * SW_BLOCK >=
+                      5 * SW_LDS_JOBS + sizeof(sw_bnb_ivl) * SW_BNB_CAP,
+                  "the staging window also holds the level search's interval list");
+    c.bnb = reinterpret_cast<sw_bnb_ivl*>(stage + 5 * NJ);
     c.placed = c.placed2 = c.nfin = nullptr;
     c.ycur = c.ybest = c.y2 = nullptr;
     c.pst = nullptr;
@@ -1643,6 +1727,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     c.placed = carve(NJ);
     c.placed2 = carve(NJ);
     c.ncur = c.lcur = c.tkcur = c.nfin = c.tiecur = nullptr;
+    c.bnb = nullptr;
     c.ycur = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
     c.ybest = nullptr;
@@ -1722,7 +1807,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
         o.p2_objective = P2;
         o.bound = lv.bound;
         o.iters = (int32_t)c.passes;
-        o.status = status;
+        o.status = status | (sw_p1_uncertified(o.objective, lv.bound) ? SW_STATUS_P1_UNCERTIFIED : 0);
         *out = o;
     }
     emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
@@ -1841,6 +1926,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.ybest = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.y2 = (uint64_t*)carve(sizeof(uint64_t) * NJ);
         c.sbuf = (uint64_t*)carve(sizeof(uint64_t) * 4 * SW_JPT * SW_BLOCK);
+        c.bnb = reinterpret_cast<sw_bnb_ivl*>(c.sbuf); /* free between the setup and each pack */
         c.gkeys = nullptr;
         c.gjc = nullptr;
         c.JL.carve(carve);
@@ -1876,9 +1962,26 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         rr_dpA = (double*)carve(8 * (SW_RR_CAPMAX + 1));
         rr_dpB = (double*)carve(8 * (SW_RR_CAPMAX + 1));
         rr_bits = (uint64_t*)carve(8 * SW_RR_WORDS);
+        /* the re-optimisation's LDS is free until the end of P1 */
+        static_assert(8 * (SW_RR_CAPMAX + 1) >= sizeof(sw_bnb_ivl) * SW_BNB_CAP, "interval list");
+        c.bnb = reinterpret_cast<sw_bnb_ivl*>(rr_dpA);
         for (int j = c.jlo(); j < c.jhi(); ++j)
             c.gjc[j] = sw_make_jobc(N, c.T, I->delta, B.w[jo + j], B.d[jo + j], B.F[jo + j],
                                     B.E[jo + j], B.R[jo + j], B.p[jo + j]);
+    }
+    /* the pattern search's scratch (pattern_pack): ONE: the sort buffer; !ONE:
+     * the re-optimisation's LDS rows when they hold it, else the workspace rows
+     * from y2 on (dead while a P1 pack is decided: 4N + 192 words) */
+    int32_t* pscr;
+    if constexpr (ONE) {
+        static_assert(8 * 4 * SW_JPT * SW_BLOCK >=
+                          4 * (SW_RCLS_MAX * (SW_TMAX + 1) + SW_PAT_SCRATCH(SW_LDS_JOBS)),
+                      "pattern scratch");
+        pscr = reinterpret_cast<int32_t*>(c.sbuf);
+    } else {
+        const int64_t need = SW_RCLS_MAX * (SW_TMAX + 1) + SW_PAT_SCRATCH((int64_t)N);
+        pscr = need <= 2 * 2 * (SW_RR_CAPMAX + 1) ? reinterpret_cast<int32_t*>(rr_dpA)
+                                                  : reinterpret_cast<int32_t*>(c.y2);
     }
     /* folds away when the carve-up matches the launch's allocation */
     if (off != sw_plan_lds_bytes(ONE)) __builtin_trap();
@@ -1943,10 +2046,26 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
                 dfc = 0;
                 rep = true;
             }
+            /* neither places: an exact class profile over round patterns
+             * (twin: pattern_pack) — the counts as they are, no re-solve */
+            bool pat = false;
+            if (dfc != 0 && c.pattern_pack(c.nbest, c.ycur, c.placed, pscr)) {
+                fs = 0.0;
+                gm = 0.0;
+                c.for_jobs([&](int j, int s) {
+                    fs = fs + c.fval(j, s, c.placed[j]);
+                    gm = sw_max(gm, c.gval(j, s, c.placed[j]));
+                });
+                c.blk.detsum_max(fs, gm, U, Mx);
+                Jo = U - c.k * Mx;
+                c.passes++;
+                dfc = 0;
+                pat = true;
+            }
             if (dfc != 0) { mode = 1; continue; }
             Jp = Jo;
             deficit = 0;
-            dens = true;
+            dens = !pat;
         } else if (mode == 1 || Jo > Jp) {
             Jp = Jo;
             deficit = dfc;
@@ -2171,7 +2290,7 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         o.p2_objective = P2;
         o.bound = bound;
         o.iters = (int32_t)c.passes;
-        o.status = status;
+        o.status = status | (sw_p1_uncertified(o.objective, bound) ? SW_STATUS_P1_UNCERTIFIED : 0);
         B.out[inst_] = o;
 #ifdef SW_STAMPS
         if (B.stamps) {

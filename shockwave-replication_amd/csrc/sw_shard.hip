@@ -652,16 +652,18 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
 /* width-class profile: red[t] = #{local j : src_j > 0, w_j = wc, bit t of
  * ys_j}; red[64] = max over local j with src_j > 0 and w_j > wc of ~w_j;
  * red[65] = #{local j : src_j > 0, w_j = wc}, red[66] = Σ over them of
- * src_j − ps_j (ps = nullptr: 0) */
+ * src_j − ps_j (ps = nullptr: 0).  hist: red[v − 1] = #{local j : src_j = v,
+ * w_j = wc} instead of the round counts (SW_CLASS_HIST) */
 __global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* src,
-                                                    const uint64_t* ys, int wc, const int32_t* ps) {
+                                                    const uint64_t* ys, int wc, const int32_t* ps,
+                                                    int hist) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     uint64_t m = 0, nx = 0;
     long long mem = 0, dfc = 0;
     if (i < S.NL && src[i] > 0) {
         const int w = S.jc[i].w;
         if (w == wc) {
-            m = ys[i];
+            m = hist ? (1ull << (src[i] - 1)) : ys[i];
             mem = 1;
             dfc = ps ? (long long)(src[i] - ps[i]) : 0;
         }
@@ -1727,7 +1729,8 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 67));
     LAUNCH(S, k_class_caps, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p,
-           S->y[ysrc].p, (int)wc, psrc >= 0 ? (const int32_t*)S->arr[psrc].p : nullptr);
+           S->y[ysrc].p, (int)wc, psrc >= 0 ? (const int32_t*)S->arr[psrc].p : nullptr,
+           (int)(psrc == SW_CLASS_HIST));
     int64_t cnt[64];
     uint64_t nx = 0;
     SH_TRY(coll_reduce(S, S->dv.red, S->T, 0, cnt));

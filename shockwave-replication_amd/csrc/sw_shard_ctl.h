@@ -42,9 +42,11 @@
 #include <string.h>
 
 #include "sw_arith.h"
+#include "sw_bnb.h"
 #include "sw_repair.h"
 
 #define SW_SHARD_K 63 /* thresholds evaluated per search step (≤ 63) */
+#define SW_CLASS_HIST (-2) /* class_caps: the class's count histogram */
 
 /* per-job count arrays an engine keeps for its jobs */
 enum {
@@ -112,6 +114,8 @@ typedef struct sw_shard_ops {
      * arr[psrc]_j (the class's unplaced rounds) */
     int (*class_caps)(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc,
                       int32_t* caps, int32_t* next_w, int64_t* md);
+    /* (psrc = SW_CLASS_HIST: caps[v − 1] = #{j : arr[src]_j = v, w_j = wc}
+     * for v = 1..T instead, the count histogram of the class; md[0] as above) */
     /* pack the jobs of width wc (arr[src] rounds, order p/n, unit widths) into
      * per-round capacities caps; writes their rows of Y[ydst] and arr[pdst]
      * and leaves every other job untouched */
@@ -336,42 +340,34 @@ static inline int swc_level_search(sw_shard_ctl* c, double* bound, double* mk) {
     }
     SWC_TRY(swc_select(c, 0.0, 1, &ev, 0, elo.rho));
     SWC_TRY(swc_keep(c, &ev, &best));
-    const uint32_t rho_inf = ev.rho;
-    const double U_inf = ev.U, M_free = ev.Mact, ub_inf = ev.ubound;
-    /* golden section with the surviving interior point reused (twin) */
-    const double width = (U_inf - elo.U) / c->k;
-    double a = M_lo, b = sw_min(M_free, M_lo + width);
-    uint32_t ra = elo.rho, rb = rho_inf;
-    nbw = 0;
-    if (a < b) {
-        SWC_TRY(o->between(o->ctx, a, b, &nbw));
+    /* branch and bound over the levels in (M_lo, M_free] (twin; sw_bnb.h) */
+    const double kk = c->k, M_free = ev.Mact;
+    double cert = sw_max(elo.ubound - kk * M_lo, ev.ubound - kk * M_free);
+    sw_bnb_ivl L[SW_BNB_CAP];
+    int32_t nL = 0, probes = 0;
+    if (M_lo < M_free) L[nL++] = sw_bnb_make(M_lo, M_free, ev.ubound, elo.rho, ev.rho);
+    while (nL > 0) {
+        double kb;
+        const int32_t i = sw_bnb_pick(L, nL, kk, &kb);
+        if (kb <= best.J) break;
+        if (probes == SW_BNB_PROBES) { cert = sw_max(cert, kb); break; }
+        const sw_bnb_ivl I = L[i];
+        L[i] = L[--nL];
+        SWC_TRY(o->between(o->ctx, I.a, I.b, &nbw));
         c->steps++;
-    }
-    if (a < b && nbw > 0) {
-        double m1 = a + (b - a) * SW_GS_A;
-        double m2 = a + (b - a) * SW_GS_B;
-        sw_shard_eval e1, e2;
-        SWC_TRY(swc_select(c, m1, 0, &e1, rb, ra));
-        SWC_TRY(swc_keep(c, &e1, &best));
-        SWC_TRY(swc_select(c, m2, 0, &e2, rb, e1.rho));
-        SWC_TRY(swc_keep(c, &e2, &best));
-        for (int it = 0; it < SW_GS_ITERS; ++it) {
-            const int left = e1.J >= e2.J;
-            if (left) { b = m2; rb = e2.rho; m2 = m1; e2 = e1; }
-            else { a = m1; ra = e1.rho; m1 = m2; e1 = e2; }
-            if (!(a < b)) break;
-            SWC_TRY(o->between(o->ctx, a, b, &nbw));
-            c->steps++;
-            if (nbw == 0) break;
-            sw_shard_eval* e = left ? &e1 : &e2;
-            double m;
-            if (left) { m1 = a + (b - a) * SW_GS_A; m = m1; }
-            else { m2 = a + (b - a) * SW_GS_B; m = m2; }
-            SWC_TRY(swc_select(c, m, 0, e, left ? e2.rho : rb, left ? ra : e1.rho));
-            SWC_TRY(swc_keep(c, e, &best));
+        if (nbw == 0) {
+            cert = sw_max(cert, I.vb - kk * I.b);
+            continue;
         }
+        const double m = sw_bnb_mid(I.a, I.b);
+        sw_shard_eval e;
+        SWC_TRY(swc_select(c, m, 0, &e, I.rb, I.ra));
+        ++probes;
+        SWC_TRY(swc_keep(c, &e, &best));
+        if (sw_bnb_key(e.ubound, kk, I.a) > best.J) L[nL++] = sw_bnb_make(I.a, m, e.ubound, I.ra, e.rho);
+        if (sw_bnb_key(I.vb, kk, m) > best.J) L[nL++] = sw_bnb_make(m, I.b, I.vb, e.rho, I.rb);
     }
-    *bound = ub_inf - c->k * M_lo;
+    *bound = sw_max(cert, best.J);
     *mk = best.Mact;
     return 0;
 }
@@ -412,6 +408,51 @@ static inline int swc_repair(sw_shard_ctl* c, int32_t nin, int32_t ysrc, int32_t
     SWC_TRY(o->copy(o->ctx, pdst, psrc));
     for (int32_t ci = 0; ci < R.ncls; ++ci) {
         if (!R.changed[ci]) continue;
+        SWC_TRY(o->pack_class(o->ctx, nin, R.wc[ci], R.caps[ci], ydst, pdst));
+        c->steps++;
+    }
+    double gm;
+    int64_t bad;
+    SWC_TRY(o->eval(o->ctx, SW_EV_UNPLACED, pdst | (nin << 8), c->lanesA, c->lanesB, &gm, &bad));
+    c->steps++;
+    *ok = bad == 0;
+    return 0;
+}
+
+/* twin: pattern_pack — an exact width-class profile over round patterns
+ * (sw_profile_search) for arr[nin], from the classes' count histograms
+ * (class_caps with psrc = SW_CLASS_HIST); every class is packed inside it
+ * into Y[ydst] / arr[pdst], which hold a pack of arr[nin] (every row with a
+ * count is rewritten).  *ok = every round placed. */
+static inline int swc_pattern(sw_shard_ctl* c, int32_t nin, int32_t ydst, int32_t pdst, int* ok) {
+    const sw_shard_ops* o = c->ops;
+    sw_repair_t R;
+    int32_t hist[SW_RCLS_MAX * (SW_TMAX + 1)];
+    int32_t caps[SW_TMAX];
+    int32_t next_w = 0, over = 0;
+    int64_t md[2] = {0, 0}, A = 0;
+    memset(&R, 0, sizeof(R));
+    *ok = 0;
+    SWC_TRY(o->class_caps(o->ctx, nin, SW_Y_CUR, 0, SW_CLASS_HIST, caps, &next_w, md));
+    c->steps++;
+    while (next_w != 0x7FFFFFFF) {
+        const int32_t wc = next_w;
+        SWC_TRY(o->class_caps(o->ctx, nin, SW_Y_CUR, wc, SW_CLASS_HIST, caps, &next_w, md));
+        c->steps++;
+        const int32_t ci = R.ncls < SW_RCLS_MAX ? sw_repair_add_class(&R, wc) : -1;
+        if (ci < 0) { over = 1; break; }
+        R.M[ci] = (int32_t)md[0];
+        A += md[0];
+        hist[ci * (c->T + 1)] = 0;
+        for (int32_t v = 1; v <= c->T; ++v) hist[ci * (c->T + 1) + v] = caps[v - 1];
+    }
+    if (over || A == 0) return 0;
+    int32_t* scratch = (int32_t*)malloc(sizeof(int32_t) * (size_t)SW_PAT_SCRATCH(A));
+    if (!scratch) return -1;
+    const int32_t found = sw_profile_search(&R, c->T, c->G, hist, scratch, NULL);
+    free(scratch);
+    if (!found) return 0;
+    for (int32_t ci = 0; ci < R.ncls; ++ci) {
         SWC_TRY(o->pack_class(o->ctx, nin, R.wc[ci], R.caps[ci], ydst, pdst));
         c->steps++;
     }
@@ -483,6 +524,16 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                         rep = 1;
                     }
                     if (dfc == 0) { Jp = Jo; dens = 1; break; }
+                    /* twin: pattern_pack — the counts as they are, no re-solve */
+                    int pok = 0;
+                    SWC_RUN(swc_pattern(c, SW_A_NB, SW_Y_CUR, SW_A_PL, &pok));
+                    if (pok) {
+                        SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                        c->steps++;
+                        Jp = sw_shard_tree(c->lanesA) - c->k * gm;
+                        deficit = 0;
+                        break;
+                    }
                     continue;
                 }
                 if (ord == 0 || Jo > Jp) {
@@ -612,6 +663,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         *makespan = gm;
         *objective = U - k * gm;
         *bound_out = bound;
+        if (sw_p1_uncertified(*objective, bound)) status |= SW_STATUS_P1_UNCERTIFIED;
         *iters = (int32_t)c->steps;
         *status_out = status;
         rc = (status & SW_STATUS_P2_FALLBACK) ? SW_FALLBACK : SW_OK;

@@ -33,6 +33,7 @@ SW_STATUS_P2_WEIGHT_ORDER = 0x8
 SW_STATUS_P2_CLASSWISE = 0x10
 SW_STATUS_P2_REPAIRED = 0x20
 SW_STATUS_P2_EXCHANGED = 0x40
+SW_STATUS_P1_UNCERTIFIED = 0x80
 
 SW_MAX_ROUNDS = 64
 SW_MAX_BASES = 8

@@ -6,7 +6,9 @@ History: first pinned with the plain price bisection (commit aed1d81), kept
 through the snapped searches (same results); re-pinned in
 round 2 when the P2 cascade gained the width-profile repair (sw_repair.h),
 which changes placements on purpose, and in round 3 when P2 gained the
-exchange step (sw_p2x.h, negative-cycle cancelling).  Performance-only changes must keep
+exchange step (sw_p2x.h, negative-cycle cancelling), and in round 5 when the level
+search became a branch and bound (sw_bnb.h) and P1 gained the pattern placement
+(sw_profile_search).  Performance-only changes must keep
 these digests; tests/test_twin_plans.py checks the twin and the GPU kernel
 against them.  Regenerate only when the algorithm is meant to change:
 
@@ -48,7 +50,7 @@ def digest(lib_path):
 
 if __name__ == "__main__":
     rows = digest(sys.argv[1])
-    json.dump({"source": "oracle/plan_twin.c, round 2 (P2 width-profile repair)", "cases": rows},
+    json.dump({"source": "oracle/plan_twin.c, round 5 (level branch and bound, pattern placement)", "cases": rows},
               open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "twin_plans.json"), "w"),
               indent=0)
     print(len(rows), "cases")

@@ -244,3 +244,21 @@ def test_gpu_shard_fuzz_host_comm(world, twin):
     for s in range(256, 256 + 48):
         a = fuzz_problem(s)
         assert_same_as_single(gpu_shard_threads(a, world), twin.solve(a), f"W={world} fuzz seed {s}")
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_gpu_shard_pattern_placement(world, rccl_solver, twin):
+    """The level search's branch and bound and the round-pattern placement on
+    the GPU engine (frag-fuzz seeds of tests/test_shard.py): RCCL at world 1,
+    host collectives at world 2, each equal to the twin bit for bit."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_frag_fuzz as mk
+
+    for s in (50115, 50417, 50439, 50104):
+        a = mk.instance(s)
+        r = rccl_solver.dist_solve(a, 0, a.N) if world == 1 else gpu_shard_threads(a, world)
+        check_plan_valid(a, r)
+        assert_same_as_single(r, twin.solve(a), f"W={world} frag seed {s}")

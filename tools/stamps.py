@@ -28,8 +28,9 @@ def main():
     lib.sw_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     cases = {
         "c3_900x30_k1e5": [ss.c3_problem(i) for i in range(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64)],
-        "g64_900x20_k1e-3": [ss.synth_problem(i, 900, 64, 20, 120.0, 1e-3, 15.0) for i in range(16)],
-        "g128_120x20_k10": [ss.synth_problem(i, 120, 128, 20, 120.0, 10.0, 5.0) for i in range(16)],
+        # scale_64gpus.json: k = 10, λ = 5; scale_128gpus.json: k = 1e-3, λ = 15
+        "g64_900x20_k10": [ss.synth_problem(i, 900, 64, 20, 120.0, 10.0, 5.0) for i in range(16)],
+        "g128_900x20_k1e-3": [ss.synth_problem(i, 900, 128, 20, 120.0, 1e-3, 15.0) for i in range(16)],
     }
     if "--c4" in sys.argv:  # the C4 instance alone (workspace path; its exchange at 10k jobs)
         cases = {"c4_10000x30": [ss.synth_problem(77, 10000, 2848, 30, 120.0, 1e5, 5.0)]}
