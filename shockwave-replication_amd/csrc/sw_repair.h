@@ -119,7 +119,10 @@ SW_HD int32_t sw_profile_repair(sw_repair_t* r, int32_t T) {
  *   S_c(k) + R·min(cap_c, k) ≥ D_c(k)  and  Σ_c w_c·max_k(D_c(k) − S_c(k)) ≤ R·G
  * with R rounds left and cap_c = min(M_c, ⌊G/w_c⌋).  It is exact up to a work
  * budget of SW_PAT_STEPS (each node costs 1 + Σ_c M_c steps, the size of its
- * Gale–Ryser check): found ⇒ a profile that places every count.
+ * Gale–Ryser check, and each pattern candidate ncls): found ⇒ a profile that
+ * places every count.  The budget bounds the one-thread search on the GPU to
+ * a few milliseconds in the worst case; it only runs for counts no order
+ * placed.
  *
  * r: ncls, wc[], M[] filled by the caller; on success r->caps[c][t] holds the
  * profile and every class is marked changed.  hist: ncls × (T + 1) ints,
@@ -128,7 +131,7 @@ SW_HD int32_t sw_profile_repair(sw_repair_t* r, int32_t T) {
  * arrays Σ_c (M_c + 1) + Σ_c (cap_c + 1) ≤ 2·A + 2·SW_RCLS_MAX).
  * Returns 1 when found, 0 when not (infeasible, or the node cap).
  */
-#define SW_PAT_STEPS (1 << 20)
+#define SW_PAT_STEPS (1 << 18)
 #define SW_PAT_SCRATCH(A) (2 * (A) + 5 * SW_RCLS_MAX)
 
 SW_HD void sw_pat_first(sw_repair_t* r, const int32_t* cap, int32_t G, int32_t t) {
@@ -143,9 +146,12 @@ SW_HD void sw_pat_first(sw_repair_t* r, const int32_t* cap, int32_t G, int32_t t
 
 /* the next maximal pattern below round t's in descending lexicographic order
  * (class ncls−1 most significant; class 0 always filled); 0 when none */
-SW_HD int32_t sw_pat_next(sw_repair_t* r, const int32_t* cap, int32_t G, int32_t t) {
+SW_HD int32_t sw_pat_next(sw_repair_t* r, const int32_t* cap, int32_t G, int32_t t,
+                          int64_t* steps) {
     const int32_t K = r->ncls;
     while (1) {
+        *steps += K; /* the budget counts every candidate, maximal or not */
+        if (*steps > SW_PAT_STEPS) return 0;
         int32_t c = 1;
         while (c < K && r->caps[c][t] == 0) ++c;
         if (c >= K) return 0;
@@ -237,8 +243,8 @@ SW_HD int32_t sw_profile_search(sw_repair_t* r, int32_t T, int32_t G, const int3
                 int32_t* h = scratch + hoff[c];
                 for (int32_t m = 1; m <= r->caps[c][t]; ++m) h[m] -= 1;
             }
-            if (sw_pat_next(r, cap, G, t)) break;
-            if (t == 0) { done = 1; break; }
+            if (sw_pat_next(r, cap, G, t, &steps)) break;
+            if (t == 0 || steps > SW_PAT_STEPS) { done = 1; break; }
             --t;
         }
         if (done) break;
