@@ -276,10 +276,10 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
  * cannot allocate (fine-grained device memory is required) or map its side,
  * every rank returns an error and keeps the init call's transport.  Results are the same bits as with RCCL or host
  * collectives.  Each rank's exchange kernel waits on the GPU for its peers,
- * so ranks that share one device must run on distinct hardware queues: with
- * several ranks of one process on ONE device, keep the process's streams at
- * or below GPU_MAX_HW_QUEUES (4 by default), or a waiting kernel can sit in
- * front of a peer's kernel in a shared queue until the timeout.
+ * so ranks that share one device must run on distinct hardware queues: more
+ * than GPU_MAX_HW_QUEUES / 2 ranks of one process on ONE device (the other
+ * half is left to the process's other streams) return SW_ERR_INVALID on
+ * every rank up front, and the init call's transport stays.
  */
 #define SW_PEER_MAX_WORLD 64
 int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs);

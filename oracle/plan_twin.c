@@ -944,20 +944,6 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
                     P.passes++;
                 }
                 if (dfc == 0) { Jp = Jo; dens = 1; break; }
-                /* neither places nb: an exact width-class profile over round
-                 * patterns, when one exists (sw_profile_search) — the counts
-                 * are P1's as they are, no re-solve; P2 then starts from (b) */
-                if (pattern_pack(&P, pr, nb, y1, placed)) {
-                    Mp = 0.0;
-                    for (int32_t j = 0; j < N; ++j) {
-                        tmp[j] = fval(&P, j, placed[j]);
-                        Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
-                    }
-                    Jp = sw_detsum(tmp, N) - P.k * Mp;
-                    P.passes++;
-                    deficit = 0;
-                    break;
-                }
                 continue;
             }
             if (ord == 0 || Jo > Jp) {
@@ -969,6 +955,19 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
                 }
             }
             if (ord == 0 && dfc == 0) break; /* order A packed everything */
+        }
+        /* no order places nb: an exact width-class profile over round
+         * patterns, when one exists (sw_profile_search) — the counts are
+         * P1's as they are, no re-solve; P2 starts from its cascade */
+        if (deficit != 0 && pattern_pack(&P, pr, nb, y1, placed)) {
+            double Mp = 0.0;
+            for (int32_t j = 0; j < N; ++j) {
+                tmp[j] = fval(&P, j, placed[j]);
+                Mp = sw_max(Mp, sw_g(&P.jc[j], placed[j]));
+            }
+            Jp = sw_detsum(tmp, N) - P.k * Mp;
+            P.passes++;
+            deficit = 0;
         }
         if (it == 0 || Jp > Jbest) {
             Jbest = Jp;

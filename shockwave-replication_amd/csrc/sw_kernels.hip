@@ -2046,26 +2046,10 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
                 dfc = 0;
                 rep = true;
             }
-            /* neither places: an exact class profile over round patterns
-             * (twin: pattern_pack) — the counts as they are, no re-solve */
-            bool pat = false;
-            if (dfc != 0 && c.pattern_pack(c.nbest, c.ycur, c.placed, pscr)) {
-                fs = 0.0;
-                gm = 0.0;
-                c.for_jobs([&](int j, int s) {
-                    fs = fs + c.fval(j, s, c.placed[j]);
-                    gm = sw_max(gm, c.gval(j, s, c.placed[j]));
-                });
-                c.blk.detsum_max(fs, gm, U, Mx);
-                Jo = U - c.k * Mx;
-                c.passes++;
-                dfc = 0;
-                pat = true;
-            }
             if (dfc != 0) { mode = 1; continue; }
             Jp = Jo;
             deficit = 0;
-            dens = !pat;
+            dens = true;
         } else if (mode == 1 || Jo > Jp) {
             Jp = Jo;
             deficit = dfc;
@@ -2078,6 +2062,20 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             }
         }
         if (mode == 1 && dfc != 0) { mode = 3; continue; }
+        /* no order places the counts: an exact class profile over round
+         * patterns (twin: pattern_pack) — the counts as they are, no re-solve */
+        if (deficit != 0 && c.pattern_pack(c.nbest, c.ycur, c.placed, pscr)) {
+            fs = 0.0;
+            gm = 0.0;
+            c.for_jobs([&](int j, int s) {
+                fs = fs + c.fval(j, s, c.placed[j]);
+                gm = sw_max(gm, c.gval(j, s, c.placed[j]));
+            });
+            c.blk.detsum_max(fs, gm, U, Mx);
+            Jp = U - c.k * Mx;
+            c.passes++;
+            deficit = 0;
+        }
         /* this repack iteration is complete */
         SW_STAMP(2);
         if (it == 0 || Jp > Jbest) {

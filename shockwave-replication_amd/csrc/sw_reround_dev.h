@@ -24,7 +24,7 @@
  *   jc(j) → sw_jobc, f(c, n), tj(j)         constants of any job, f, schedulable
  *   y(j) (u64&), cnt(j), add_cnt(j, d)      the plan's masks and counts
  *   V/H0/H1(j, s) (double&)                 per-job values of the round
- *   S, Sb (uint8_t*, per job), items (u32: w << 16 | j), iv (double),
+ *   S, Sb (uint8_t*, per job), items (u32: the job index), iv (double),
  *   dpA, dpB (SW_RR_CAPMAX + 1 doubles), bits (SW_RR_WORDS words).
  */
 #pragma once
@@ -79,7 +79,7 @@ __device__ __forceinline__ bool sw_rr_knap(Env& e, Cand&& cand, int64_t cap, int
     int p = base;
     e.for_jobs([&](int j, int s) {
         if (cand(j, s)) {
-            e.items[p] = ((uint32_t)e.jc(j).w << 16) | (uint32_t)j;
+            e.items[p] = (uint32_t)j; /* the full job index; its width is read back from jc */
             e.iv[p] = e.V(j, s);
             ++p;
         }
@@ -90,8 +90,7 @@ __device__ __forceinline__ bool sw_rr_knap(Env& e, Cand&& cand, int64_t cap, int
     double* nxt = e.dpB;
     const int span = nw * 64; /* whole words: a wave's lanes share one */
     for (int i = 0; i < NI; ++i) {
-        const uint32_t it = e.items[i];
-        const int w = (int)(it >> 16);
+        const int w = e.jc((int)e.items[i]).w;
         const double v = e.iv[i];
         for (int c = tid; c < span; c += NT) {
             bool tk = false;
@@ -128,9 +127,9 @@ __device__ __forceinline__ bool sw_rr_knap(Env& e, Cand&& cand, int64_t cap, int
         int c = cs;
         for (int i = NI - 1; i >= 0; --i)
             if ((e.bits[(size_t)i * nw + (c >> 6)] >> (c & 63)) & 1ull) {
-                const uint32_t it = e.items[i];
-                e.S[it & 0xFFFFu] = 1;
-                c -= (int)(it >> 16);
+                const int j = (int)e.items[i];
+                e.S[j] = 1;
+                c -= e.jc(j).w;
             }
     }
     __syncthreads();

@@ -2062,6 +2062,25 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
     }
     long long ok = 1;
     for (int32_t p = 0; p < W; ++p) ok &= all[(size_t)p].ok;
+    /* Ranks of this process on this device wait for each other INSIDE their
+     * exchange kernels, so each needs a hardware queue of its own: a waiting
+     * kernel queued in front of a peer's kernel blocks it until the timeout.
+     * HIP maps a process's streams round robin onto GPU_MAX_HW_QUEUES queues
+     * (4 by default), and the process holds other streams too (the handles'
+     * copy streams, torch's, RCCL's), so at most half of them may carry
+     * same-device ranks: more is refused up front, on every rank alike. */
+    int32_t same = 0;
+    for (int32_t p = 0; p < W; ++p)
+        same += all[(size_t)p].nonce[0] == mine.nonce[0] && all[(size_t)p].nonce[1] == mine.nonce[1] &&
+                memcmp(all[(size_t)p].boot, mine.boot, sizeof(mine.boot)) == 0 &&
+                all[(size_t)p].device == mine.device;
+    int32_t hwq = 4;
+    if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
+        const int v = atoi(e);
+        if (v > 0) hwq = v;
+    }
+    const bool queues_short = same > 1 && same > hwq / 2;
+    if (queues_short) ok = 0;
     for (int32_t p = 0; p < W && ok; ++p) {
         if (p == S->rank) {
             S->ps.base[p] = S->xreg;
@@ -2089,12 +2108,24 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
             S->ps.base[p] = (unsigned char*)q;
         }
     }
+    /* 1 = mapped, 0 = could not map, -1 = refused for lack of hardware queues */
+    long long st = queues_short ? -1 : ok;
     std::vector<long long> oks((size_t)W);
     {
-        const int rc = gather(&ok, oks.data(), sizeof(long long));
+        const int rc = gather(&st, oks.data(), sizeof(long long));
         if (rc < 0) { undo(); return rc; }
     }
-    for (int32_t p = 0; p < W; ++p) ok &= oks[(size_t)p];
+    bool refused = false;
+    for (int32_t p = 0; p < W; ++p) {
+        refused |= oks[(size_t)p] < 0;
+        ok &= oks[(size_t)p] > 0;
+    }
+    if (refused) {
+        undo();
+        return h->err = "peer transport: more same-device ranks in one process than half of "
+                        "GPU_MAX_HW_QUEUES (init transport kept)",
+               SW_ERR_INVALID;
+    }
     if (!ok) {
         undo();
         return h->err = "peer transport: a rank could not map the exchange regions (init transport kept)",

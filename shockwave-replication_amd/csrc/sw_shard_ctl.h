@@ -524,16 +524,6 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                         rep = 1;
                     }
                     if (dfc == 0) { Jp = Jo; dens = 1; break; }
-                    /* twin: pattern_pack — the counts as they are, no re-solve */
-                    int pok = 0;
-                    SWC_RUN(swc_pattern(c, SW_A_NB, SW_Y_CUR, SW_A_PL, &pok));
-                    if (pok) {
-                        SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
-                        c->steps++;
-                        Jp = sw_shard_tree(c->lanesA) - c->k * gm;
-                        deficit = 0;
-                        break;
-                    }
                     continue;
                 }
                 if (ord == 0 || Jo > Jp) {
@@ -545,6 +535,17 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                     }
                 }
                 if (ord == 0 && dfc == 0) break;
+            }
+            if (deficit != 0) { /* twin: pattern_pack — the counts as they are */
+                int pok = 0;
+                SWC_RUN(swc_pattern(c, SW_A_NB, SW_Y_CUR, SW_A_PL, &pok));
+                if (pok) {
+                    int64_t dfc;
+                    SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                    c->steps++;
+                    Jp = sw_shard_tree(c->lanesA) - c->k * gm;
+                    deficit = 0;
+                }
             }
             if (it == 0 || Jp > Jbest) {
                 Jbest = Jp;

@@ -321,7 +321,11 @@ EXPORTED_SYMBOLS = (
 
 
 class NativeError(RuntimeError):
-    pass
+    """A negative return code of the C-ABI; .code holds it."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 _LIB = None
@@ -420,7 +424,7 @@ class Solver:
 
     def _check(self, rc, what):
         if rc < 0:
-            raise NativeError(f"{what} failed ({rc}): {self.error()}")
+            raise NativeError(f"{what} failed ({rc}): {self.error()}", rc)
         return rc
 
     def solve(self, arrays: ProblemArrays) -> dict:

@@ -262,3 +262,48 @@ def test_gpu_shard_pattern_placement(world, rccl_solver, twin):
         r = rccl_solver.dist_solve(a, 0, a.N) if world == 1 else gpu_shard_threads(a, world)
         check_plan_valid(a, r)
         assert_same_as_single(r, twin.solve(a), f"W={world} frag seed {s}")
+
+
+def test_gpu_shard_peer_refuses_too_many_same_device_ranks(twin):
+    """Four ranks of one process on one device exceed half of the process's
+    hardware queues (GPU_MAX_HW_QUEUES = 4 on the box): sw_dist_enable_peer
+    refuses on every rank with SW_ERR_INVALID at once (no 10 s timeout), and
+    the init call's transport (host collectives) still solves, equal to the
+    twin."""
+    import time
+
+    world = 4
+    case = CASES[1]
+    seed, N, G, T, k, lam = case
+    a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
+    group = ThreadGroup(world)
+    codes = [None] * world
+    out = [None] * world
+    errs = []
+
+    def work(r):
+        try:
+            s = sn.Solver(device=0)
+            s.dist_init_host(sn.HostComm(group.member(r)), r, world)
+            try:
+                s.dist_enable_peer(a.N)
+                codes[r] = 0
+            except sn.NativeError as e:
+                codes[r] = e.code
+            lo, hi = sn.shard_range(a.N, world, r)
+            out[r] = (lo, hi, s.dist_solve(a.slice(lo, hi), lo, a.N))
+            s.close()
+        except Exception as e:
+            errs.append(e)
+            group.barrier.abort()
+
+    t0 = time.time()
+    ths = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    assert codes == [sn.SW_ERR_INVALID] * world, codes
+    assert time.time() - t0 < 60
+    assert_same_as_single(assemble(a, out), twin.solve(a), "after the refusal")
