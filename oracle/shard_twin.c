@@ -22,6 +22,7 @@
 
 #include "../include/shockwave_amd.h"
 #include "../shockwave-replication_amd/csrc/sw_arith.h"
+#include "../shockwave-replication_amd/csrc/sw_repair.h"
 #include "../shockwave-replication_amd/csrc/sw_shard_ctl.h"
 #include "../shockwave-replication_amd/csrc/sw_validate.h"
 
@@ -46,6 +47,8 @@ typedef struct {
     int32_t* arr[SW_A_COUNT];
     uint64_t* y[SW_Y_COUNT];
     int32_t* w_all;
+    int32_t scaps[SW_TMAX]; /* this rank's share of every round (pack_share) */
+    int share;              /* the shares exist (sw_share_caps succeeded) */
     sw_result* res;
 } eng_t;
 
@@ -427,6 +430,103 @@ static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_
     return 0;
 }
 
+/* the share placement (sw_shard_ops.pack_share): loads all-gathered, this
+ * rank's jobs packed alone into its shares of the rounds (density order,
+ * mixed widths, the tier rule over non-uniform capacities: plan_twin.c pack) */
+static int e_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
+    eng_t* E = (eng_t*)ctx;
+    const int32_t NL = E->NL, T = E->T;
+    const size_t NN = NL > 0 ? (size_t)NL : 1;
+    int64_t mine = 0;
+    for (int32_t i = 0; i < NL; ++i) mine += (int64_t)E->jc[i].w * E->arr[src][i];
+    int64_t* loads = (int64_t*)calloc((size_t)E->world, sizeof(int64_t));
+    int32_t* w = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* nin = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
+    uint32_t* k2 = (uint32_t*)calloc(NN, sizeof(uint32_t));
+    int32_t* placed = (int32_t*)calloc(NN, sizeof(int32_t));
+    uint8_t* y = (uint8_t*)calloc(NN * (size_t)T, 1);
+    int rc = -1;
+    if (!loads || !w || !nin || !k1 || !k2 || !placed || !y) goto out;
+    rc = E->comm->allgather(E->comm->ctx, &mine, loads, (int64_t)sizeof(int64_t));
+    if (rc) goto out;
+    E->share = sw_share_caps(loads, E->world, E->rank, T, E->G, E->scaps) == 0;
+    for (int32_t i = 0; i < NL; ++i) {
+        w[i] = E->jc[i].w;
+        nin[i] = E->share ? E->arr[src][i] : 0;
+        k1[i] = nin[i] > 0 ? sw_ratio_key(E->p[i] / (double)(nin[i] * w[i])) : 0;
+    }
+    if (E->share) twin_pack_arrays_caps(NL, T, E->G, w, nin, k1, k2, y, placed, E->scaps, 0);
+    for (int32_t i = 0; i < NL; ++i) {
+        uint64_t m = 0;
+        for (int32_t t = 0; t < T; ++t) m |= (uint64_t)y[(size_t)i * T + t] << t;
+        E->y[ydst][i] = m;
+        E->arr[pdst][i] = placed[i];
+    }
+out:
+    free(loads); free(w); free(nin); free(k1); free(k2); free(placed); free(y);
+    return rc;
+}
+
+/* sw_shard_ops.share_repair: when this rank's share pack stranded rounds,
+ * its width profile is repaired inside its shares (sw_profile_repair with
+ * the shares' free GPUs) and every changed class is repacked alone (unit
+ * widths, order p/n) — plan_twin.c repair_pack on the rank's own jobs */
+static int e_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
+    eng_t* E = (eng_t*)ctx;
+    const int32_t NL = E->NL, T = E->T;
+    if (!E->share) return 0;
+    int64_t dfc = 0;
+    for (int32_t i = 0; i < NL; ++i) dfc += (int64_t)E->jc[i].w * (E->arr[src][i] - E->arr[pdst][i]);
+    if (dfc == 0) return 0;
+    sw_repair_t R;
+    memset(&R, 0, sizeof(R));
+    for (int32_t i = 0; i < NL; ++i)
+        if (E->arr[src][i] > 0 && sw_repair_add_class(&R, E->jc[i].w) < 0) return 0;
+    for (int32_t t = 0; t < T; ++t) R.L[t] = E->scaps[t];
+    for (int32_t i = 0; i < NL; ++i) {
+        const uint64_t m = E->y[ydst][i];
+        for (int32_t t = 0; t < T; ++t)
+            if ((m >> t) & 1u) R.L[t] -= E->jc[i].w;
+        if (E->arr[src][i] <= 0) continue;
+        const int32_t c = sw_repair_class(&R, E->jc[i].w);
+        R.M[c] += 1;
+        R.D[c] += E->arr[src][i] - E->arr[pdst][i];
+        for (int32_t t = 0; t < T; ++t) R.caps[c][t] += (int32_t)((m >> t) & 1u);
+    }
+    if (sw_profile_repair(&R, T) != 0) return 0;
+    const size_t NN = NL > 0 ? (size_t)NL : 1;
+    int32_t* w = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* nc = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
+    uint32_t* k2 = (uint32_t*)calloc(NN, sizeof(uint32_t));
+    int32_t* pc = (int32_t*)calloc(NN, sizeof(int32_t));
+    uint8_t* yc = (uint8_t*)calloc(NN * (size_t)T, 1);
+    int rc = -1;
+    if (!w || !nc || !k1 || !k2 || !pc || !yc) goto out;
+    for (int32_t i = 0; i < NL; ++i) w[i] = E->jc[i].w;
+    for (int32_t c = 0; c < R.ncls; ++c) {
+        if (!R.changed[c]) continue;
+        for (int32_t i = 0; i < NL; ++i) {
+            const int cls = E->arr[src][i] > 0 && w[i] == R.wc[c];
+            nc[i] = cls ? E->arr[src][i] : 0;
+            k1[i] = cls ? sw_ratio_key(E->p[i] / (double)nc[i]) : 0;
+        }
+        twin_pack_arrays_caps(NL, T, E->G, w, nc, k1, k2, yc, pc, R.caps[c], 1);
+        for (int32_t i = 0; i < NL; ++i) {
+            if (nc[i] <= 0) continue;
+            uint64_t m = 0;
+            for (int32_t t = 0; t < T; ++t) m |= (uint64_t)yc[(size_t)i * T + t] << t;
+            E->y[ydst][i] = m;
+            E->arr[pdst][i] = pc[i];
+        }
+    }
+    rc = 0;
+out:
+    free(w); free(nc); free(k1); free(k2); free(pc); free(yc);
+    return rc;
+}
+
 /* the P2 exchange step on the gathered placement (twin_p2x_run) */
 int32_t twin_p2x_run(int32_t A, int32_t T, int32_t G, const int32_t* job, const int32_t* w,
                      const double* c, uint64_t* m);
@@ -590,6 +690,8 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.p2x = e_p2x;
     ops.reround = e_reround;
     ops.search = NULL; /* the controller's own K-ary loop */
+    ops.pack_share = e_pack_share;
+    ops.share_repair = e_share_repair;
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,
                             &res->status);

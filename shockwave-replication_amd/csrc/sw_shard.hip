@@ -77,6 +77,10 @@ constexpr int kTB = 256;  /* threads per block of the per-job kernels */
 constexpr int kRed = 128; /* entries of the step-result buffer        */
 constexpr int kRing = 64; /* step-result slices cleared together      */
 constexpr int kProbeBlocks = 256; /* grid of the K-ary probe kernels       */
+/* capacity rows a pack stages (pinned host row → device row, asynchronous):
+ * a row is rewritten kCapsRows packs later, and at most 8 class packs plus
+ * one share pack are enqueued between two host-synchronised steps */
+constexpr uint32_t kCapsRows = 16;
 
 struct sw_pack_ent {
     uint64_t khi, klo; /* order key (desc); klo low 32 bits = ~job */
@@ -675,6 +679,14 @@ __global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* s
     red_add(S.red + 66, dfc);
 }
 
+/* this rank's load Σ w·src (the share placement) → red[0] */
+__global__ __launch_bounds__(kTB) void k_load(ShardDev S, const int32_t* src) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    long long v = 0;
+    if (i < S.NL) v = (long long)S.jc[i].w * src[i];
+    red_add(S.red, v);
+}
+
 /* per-solve state: every count array, every bitmask, l and taken = 0 */
 __global__ __launch_bounds__(kTB) void k_zero_state(ShardDev S) {
     const int i = blockIdx.x * kTB + threadIdx.x;
@@ -810,7 +822,7 @@ template <int E, int NT>
 __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
                                                     int64_t M, const int32_t* order,
                                                     uint64_t* ydst, int32_t* pdst,
-                                                    const int32_t* capsd, int alo) {
+                                                    const int32_t* capsd, int alo, int zero) {
     __shared__ sw_xchg_t<NT / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
@@ -823,7 +835,7 @@ __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_en
     for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
     if (A <= alo || A > E * NT) return; /* the other variant places these */
-    if (!capsd)
+    if (zero) /* a whole placement (not one width class): every row of this rank */
         for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
     pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
 }
@@ -1218,6 +1230,9 @@ struct sw_shard_state {
     /* pinned staging */
     HostBuf<uint8_t> hx;
     HostBuf<int32_t> hcaps;
+    uint32_t caps_row = 0; /* next staging row of hcaps / caps (pack_any) */
+    int32_t scaps[SW_TMAX]; /* this rank's share of every round (op_pack_share) */
+    bool share = false;
     std::vector<int32_t> w_all;
     std::vector<uint8_t> hgather;
 };
@@ -1665,21 +1680,27 @@ int op_copy_y(void* ctx, int32_t dst, int32_t src) {
     return SW_OK;
 }
 
+/* local: the share placement — only this rank's entries, no gather, caps is
+ * this rank's share of every round (mode 4) or its class capacities (mode 5) */
 int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
-             int32_t wc, const int32_t* caps) {
+             int32_t wc, const int32_t* caps, bool local = false) {
     hipStream_t st = S->h->stream;
-    const int64_t M = S->P * S->world;
+    const int64_t M = local ? S->P : S->P * S->world;
     const int32_t* capsd = nullptr;
-    if (mode == 5) {
-        memcpy(S->hcaps.p, caps, (size_t)S->T * 4);
-        SH_HIP(S, hipMemcpyAsync(S->caps.p, S->hcaps.p, (size_t)S->T * 4, hipMemcpyHostToDevice, st));
-        capsd = S->caps.p;
+    if (caps) {
+        /* a staging row of its own (kCapsRows), so no synchronisation */
+        int32_t* hc = S->hcaps.p + (size_t)(S->caps_row++ % kCapsRows) * 64;
+        memcpy(hc, caps, (size_t)S->T * 4);
+        int32_t* dc = S->caps.p + (size_t)((S->caps_row - 1) % kCapsRows) * 64;
+        SH_HIP(S, hipMemcpyAsync(dc, hc, (size_t)S->T * 4, hipMemcpyHostToDevice, st));
+        capsd = dc;
     }
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
            (int)wc, S->pall.p + (size_t)S->rank * S->P);
-    const void* gv = nullptr; /* in-place all-gather: the keys go straight to this rank's block */
-    SH_TRY(coll_gather(S, S->pall.p + (size_t)S->rank * S->P, S->pall.p,
-                       (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
+    const void* gv = S->pall.p + (size_t)S->rank * S->P;
+    if (!local) /* in-place all-gather: the keys go straight to this rank's block */
+        SH_TRY(coll_gather(S, S->pall.p + (size_t)S->rank * S->P, S->pall.p,
+                           (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
     const sw_pack_ent* all = (const sw_pack_ent*)gv;
     const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
     LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, all, M, S->skeys.p,
@@ -1693,7 +1714,7 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
      * variant, for instances whose active jobs fit it (k_pack_rounds) */
 #define SW_LAUNCH_PACK(E, NT, ALO)                                                              \
     LAUNCH(S, (k_pack_rounds<E, NT>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, \
-           pd, capsd, (int)(ALO))
+           pd, capsd, (int)(ALO), (int)(mode != 5))
     if (M <= 2 * SW_BLOCK) {
         SW_LAUNCH_PACK(2, SW_BLOCK, -1);
     } else if (M <= 8 * SW_BLOCK) {
@@ -1711,12 +1732,67 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
     }
 #undef SW_LAUNCH_PACK
-    if (mode == 5) SH_HIP(S, hipStreamSynchronize(st)); /* hcaps is reused by the next class */
     return SW_OK;
 }
 
 int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst) {
     return pack_any((sw_shard_state*)ctx, mode, src, Mb, ydst, pdst, 0, nullptr);
+}
+
+/* twin: e_pack_share (oracle/shard_twin.c) — the ranks' loads all-gathered,
+ * this rank's jobs placed alone in its shares (sw_share_caps) */
+int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 1));
+    LAUNCH(S, k_load, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p);
+    std::vector<int64_t> loads((size_t)S->world);
+    SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 8, loads.data()));
+    S->share = sw_share_caps(loads.data(), S->world, S->rank, S->T, S->dv.G, S->scaps) == 0;
+    if (!S->share) { /* nothing placed: the gathered orders decide */
+        SH_HIP(S, hipMemsetAsync(S->y[ydst].p, 0, (size_t)S->NL * 8, S->h->stream));
+        SH_HIP(S, hipMemsetAsync(S->arr[pdst].p, 0, (size_t)S->NL * 4, S->h->stream));
+        return SW_OK;
+    }
+    return pack_any(S, 4, src, 0.0, ydst, pdst, 0, S->scaps, true);
+}
+
+/* twin: e_share_repair — this rank's width profile repaired inside its shares
+ * (host: sw_profile_repair), every changed class repacked alone (local) */
+int op_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
+    auto* S = (sw_shard_state*)ctx;
+    if (!S->share || S->NL <= 0) return SW_OK;
+    const int32_t NL = S->NL, T = S->T;
+    std::vector<uint64_t> y((size_t)NL);
+    std::vector<int32_t> n((size_t)NL), pl((size_t)NL), w((size_t)NL);
+    hipStream_t st = S->h->stream;
+    SH_HIP(S, hipMemcpyAsync(y.data(), S->y[ydst].p, (size_t)NL * 8, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipMemcpyAsync(n.data(), S->arr[src].p, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipMemcpyAsync(pl.data(), S->arr[pdst].p, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipMemcpyAsync(w.data(), S->in_w, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
+    SH_HIP(S, hipStreamSynchronize(st));
+    int64_t dfc = 0;
+    for (int32_t i = 0; i < NL; ++i) dfc += (int64_t)w[i] * (n[i] - pl[i]);
+    if (dfc == 0) return SW_OK;
+    sw_repair_t R;
+    memset(&R, 0, sizeof(R));
+    for (int32_t i = 0; i < NL; ++i)
+        if (n[i] > 0 && sw_repair_add_class(&R, w[i]) < 0) return SW_OK;
+    for (int32_t t = 0; t < T; ++t) R.L[t] = S->scaps[t];
+    for (int32_t i = 0; i < NL; ++i) {
+        for (int32_t t = 0; t < T; ++t)
+            if ((y[i] >> t) & 1u) R.L[t] -= w[i];
+        if (n[i] <= 0) continue;
+        const int32_t c = sw_repair_class(&R, w[i]);
+        R.M[c] += 1;
+        R.D[c] += n[i] - pl[i];
+        for (int32_t t = 0; t < T; ++t) R.caps[c][t] += (int32_t)((y[i] >> t) & 1u);
+    }
+    if (sw_profile_repair(&R, T) != 0) return SW_OK;
+    for (int32_t c = 0; c < R.ncls; ++c) {
+        if (!R.changed[c]) continue;
+        SH_TRY(pack_any(S, 5, src, 0.0, ydst, pdst, R.wc[c], R.caps[c], true));
+    }
+    return SW_OK;
 }
 
 int op_pack_class(void* ctx, int32_t src, int32_t wc, const int32_t* caps, int32_t ydst,
@@ -1819,7 +1895,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
-               S->porder.reserve(M) || S->caps.reserve(64) || S->hcaps.reserve(64) ||
+               S->porder.reserve(M) || S->caps.reserve(64 * kCapsRows) || S->hcaps.reserve(64 * kCapsRows) ||
                S->srch.reserve(8) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
@@ -2190,6 +2266,8 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.p2x = op_p2x;
     ops.reround = op_reround;
     ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
+    ops.pack_share = op_pack_share;
+    ops.share_repair = op_share_repair;
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,
                             &res->p2_objective, &res->bound, &res->iters, &res->status);

@@ -143,6 +143,15 @@ typedef struct sw_shard_ops {
      * rounds (collective steps) it took, which must equal swc_search's */
     int (*search)(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
                   int32_t* rounds);
+    /* the share placement: the ranks' loads Σ w·arr[src]
+     * are all-gathered, sw_share_caps gives this rank its share of every
+     * round's capacity, and the rank places its own jobs there alone
+     * (density order p/(n·w), the tier rule over its per-round shares) into
+     * Y[ydst] / arr[pdst] — no gathered placement.  share_repair repairs
+     * this rank's width profile inside its shares (sw_profile_repair) when
+     * the pack stranded rounds of its own jobs; no collective. */
+    int (*pack_share)(void* ctx, int32_t src, int32_t ydst, int32_t pdst);
+    int (*share_repair)(void* ctx, int32_t src, int32_t ydst, int32_t pdst);
 } sw_shard_ops;
 
 /* Job range of `rank` (sw_dist_shard_range in include/shockwave_amd.h). */
@@ -155,6 +164,44 @@ static inline int sw_shard_range(int64_t N, int32_t world, int32_t rank, int64_t
     int64_t a = (int64_t)rank * per, b = a + per;
     *lo = a < N ? a : N;
     *hi = b < N ? b : N;
+    return 0;
+}
+
+/*
+ * The share placement's per-round capacities of rank `rank`.
+ * loads[r] = Σ w_j·n_j over rank r's jobs, L = Σ_r loads[r] ≤ G·T.  Rank r's
+ * budget is B_r = loads[r] + its share of the slack S = G·T − L: ⌊S·L_r/L⌋,
+ * and one more unit for each of the first S − Σ_r ⌊S·L_r/L⌋ ranks.  It gets
+ * ⌊B_r/T⌋ GPUs in every round and one more in B_r mod T rounds; those
+ * extras are one stream over the ranks in rank order (rank r's start at
+ * round Σ_{r' < r} (B_r' mod T) mod T and wrap), and Σ_r B_r = G·T, so every
+ * round's shares sum to exactly G.  Each rank then holds at least its own
+ * load, spread like the whole instance's capacity (flat, so its density
+ * order front-loads its jobs as the whole instance's would).  At world 1 the
+ * share is G in every round: the single-instance pack.  Returns 0, or -1
+ * when L = 0 or L > G·T (no share placement).
+ */
+static inline int sw_share_caps(const int64_t* loads, int32_t W, int32_t rank, int32_t T, int64_t G,
+                                int32_t* caps) {
+    __int128 L = 0;
+    for (int32_t r = 0; r < W; ++r) L += loads[r];
+    const __int128 C = (__int128)G * T;
+    if (L <= 0 || L > C || T < 1) return -1;
+    const __int128 S = C - L;
+    __int128 given = 0;
+    for (int32_t r = 0; r < W; ++r) given += S * loads[r] / L;
+    const int64_t rest = (int64_t)(S - given); /* < W */
+    int64_t cursor = 0, Bme = 0;
+    for (int32_t r = 0; r <= rank; ++r) {
+        const int64_t B = loads[r] + (int64_t)(S * loads[r] / L) + (r < rest ? 1 : 0);
+        if (r < rank) cursor = (cursor + B % T) % T;
+        else Bme = B;
+    }
+    const int64_t base = Bme / T, ext = Bme % T;
+    for (int32_t t = 0; t < T; ++t) {
+        const int64_t d = ((int64_t)t - cursor + T) % T; /* position in this rank's extras */
+        caps[t] = (int32_t)(base + (d < ext ? 1 : 0));
+    }
     return 0;
 }
 
@@ -503,7 +550,32 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             int64_t deficit = 0;
             double Jp = 0.0;
             int dens = 0, rep = 0;
-            for (int ord = -1; ord < 2; ++ord) {
+            /* the share placement: every rank places its own jobs in its share
+             * of each round (no gathered placement); it is P1's and, in density
+             * order, P2's.  When it strands rounds on some rank, that rank
+             * repairs its profile; if rounds stay unplaced, the gathered orders
+             * below decide (the single-instance flow) */
+            int ord0 = -1;
+            if (o->pack_share) {
+                int64_t dfc;
+                SWC_RUN(o->pack_share(o->ctx, SW_A_NB, SW_Y_CUR, SW_A_PL));
+                c->steps++;
+                SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                c->steps++;
+                const int repaired = dfc != 0; /* twin: the density pack's repair */
+                if (dfc != 0) {
+                    SWC_RUN(o->share_repair(o->ctx, SW_A_NB, SW_Y_CUR, SW_A_PL));
+                    SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                    c->steps++;
+                }
+                if (dfc == 0) {
+                    Jp = sw_shard_tree(c->lanesA) - c->k * gm;
+                    dens = 1;
+                    rep = repaired;
+                    ord0 = 2; /* placed: no gathered order */
+                }
+            }
+            for (int ord = ord0; ord < 2; ++ord) {
                 const int32_t pdst = ord == 1 ? SW_A_PL2 : SW_A_PL;
                 const int32_t pm = ord < 0 ? 4 : ord ? 3 : 1;
                 SWC_RUN(o->pack(o->ctx, pm, SW_A_NB, Mb, ord == 1 ? SW_Y_2 : SW_Y_CUR, pdst));

@@ -1,8 +1,10 @@
-"""Generate tests/golden/c4_digest.json: the CPU twin's solve (oracle/plan_twin.c,
-the bit-exact restatement of the GPU algorithm) of the C4 instance that
-bench.py's c4_sharded sub-record solves sharded over N GPUs.  bench.py checks
-its gathered plan / counts / objective against these digests at every N
-(the sharded solve returns the single-instance result bit for bit).
+"""Generate tests/golden/c4_digest.json: the CPU solves of the C4 instance that
+bench.py's c4_sharded sub-record solves sharded over N GPUs — the twin
+(oracle/plan_twin.c, the single-instance solve, = the sharded solve at world 1)
+and the CPU shard engine (oracle/shard_twin.c, the specification of the GPU
+shard engine) at worlds 2, 4 and 8, where the share placement makes the plan
+rows depend on the world size.  bench.py checks its gathered
+plan / counts / objective against the digest of its world size.
 
     python tests/golden/make_c4_digest.py
 """
@@ -34,6 +36,24 @@ def main():
            "plan_sha": hashlib.sha256(a.plan.tobytes()).hexdigest()[:32],
            "counts_sha": hashlib.sha256(a.planned.astype(sn.np.int32).tobytes()).hexdigest()[:32],
            "objective_hex": float(res.objective).hex(), "status": res.status, "iters": res.iters}
+    sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+    import test_shard as ts  # noqa: E402
+
+    slib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libplan_twin.so"))
+    slib.shard_twin_solve.argtypes = [ctypes.POINTER(sn.SwHostComm), ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(sn.SwProblem), ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.POINTER(sn.SwResult)]
+    slib.shard_twin_solve.restype = ctypes.c_int
+    by = {}
+    for W in (1, 2, 4, 8):
+        r = ts.run_threads(slib, a, W)
+        by[str(W)] = {"plan_sha": hashlib.sha256(sn.np.ascontiguousarray(r["plan"]).tobytes()).hexdigest()[:32],
+                      "counts_sha": hashlib.sha256(sn.np.ascontiguousarray(r["planned_rounds"],
+                                                                          dtype=sn.np.int32).tobytes()).hexdigest()[:32],
+                      "objective_hex": float(r["objective"]).hex(),
+                      "p2_objective": float(r["p2_objective"]), "status": int(r["status"])}
+    assert by["1"]["plan_sha"] == out["plan_sha"] and by["1"]["objective_hex"] == out["objective_hex"]
+    out["by_world"] = by
     json.dump(out, open(OUT, "w"), indent=1)
     print(out)
 

@@ -1,7 +1,9 @@
-"""The committed C4 digest (tests/golden/c4_digest.json) that bench.py's
-c4_sharded sub-record checks at every N is the CPU twin's solve of that
-instance (so a stale digest fails here, on the CPU, before a GPU run); and on
-the GPU the RCCL-sharded engine at world 1 reproduces it."""
+"""The committed C4 digests (tests/golden/c4_digest.json) that bench.py's
+c4_sharded sub-record checks at every N are the CPU solves of that instance —
+the twin's at world 1, the CPU shard engine's at worlds 2, 4, 8 (DESIGN.md
+§7.2: the share placement's rows depend on W) — so a stale digest fails here,
+on the CPU, before a GPU run; and on the GPU the RCCL-sharded engine at world
+1 reproduces the world-1 digest."""
 import hashlib
 import json
 import os
@@ -49,6 +51,30 @@ def test_c4_digest_is_the_twin_solve(twin):
     r = twin.solve(a)
     assert digest(r["plan"], r["planned_rounds"]) == (GOLD["plan_sha"], GOLD["counts_sha"])
     assert float(r["objective"]).hex() == GOLD["objective_hex"]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_c4_world_digests_are_the_shard_engine(world, twin):
+    """The CPU shard engine at W (threads) reproduces the committed digest of W,
+    and keeps the single-instance P1 objective (the share placement places
+    every count); its P2 stays within the contract's ratio."""
+    import ctypes
+
+    import sw_native as sn
+    import test_shard as ts
+    from conftest import TWIN_SO
+
+    lib = ctypes.CDLL(TWIN_SO)
+    lib.shard_twin_solve.argtypes = [ctypes.POINTER(sn.SwHostComm), ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.POINTER(sn.SwProblem), ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(sn.SwResult)]
+    lib.shard_twin_solve.restype = ctypes.c_int
+    a = c4()
+    r = ts.run_threads(lib, a, world)
+    g = GOLD["by_world"][str(world)]
+    assert digest(r["plan"], r["planned_rounds"]) == (g["plan_sha"], g["counts_sha"])
+    assert float(r["objective"]).hex() == g["objective_hex"] == GOLD["objective_hex"]
+    ts.assert_share_contract(r, twin.solve(a), f"C4 W={world}")
 
 
 def test_c4_objective_within_lp_bound(twin):

@@ -3,9 +3,11 @@
 The box has one MI355X, so multi-rank runs put W handles on cuda:0 as threads
 of this process with host collectives (a barrier-based allgather); the
 world-1 run goes through RCCL (ncclAllReduce / ncclAllGather on the handle's
-stream).  Every run must return exactly the single-instance result of the CPU
-twin (oracle/plan_twin.c) — which the batched GPU kernel also matches — for
-plan rows, counts and the bits of every objective.
+stream).  Every run must return exactly the CPU shard engine's result at the
+same world size (oracle/shard_twin.c, ranks as threads: tests/test_shard.py)
+for plan rows, counts and the bits of every objective — at world 1 that is
+the single-instance twin's (oracle/plan_twin.c), which the batched GPU kernel
+also matches; above it the share placement's.
 """
 import threading
 
@@ -15,7 +17,8 @@ import pytest
 import sw_native as sn
 import sw_synth as ss
 from helpers import check_plan_valid
-from test_shard import CASES, ThreadGroup, assemble, assert_same_as_single
+from test_shard import (CASES, ThreadGroup, assemble, assert_same_as_single, run_threads,  # noqa: F401
+                        shard_lib)
 
 pytestmark = pytest.mark.gpu
 
@@ -67,12 +70,12 @@ def test_gpu_shard_rccl_world1(case, rccl_solver, twin):
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("case", [CASES[1], CASES[4], CASES[6], CASES[7]],
                          ids=["N50", "N300_T64", "N900", "N1500"])
-def test_gpu_shard_host_comm(case, world, twin):
+def test_gpu_shard_host_comm(case, world, shard_lib):
     seed, N, G, T, k, lam = case
     a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
     r = gpu_shard_threads(a, world)
     check_plan_valid(a, r)
-    assert_same_as_single(r, twin.solve(a), f"W={world} {case}")
+    assert_same_as_single(r, run_threads(shard_lib, a, world), f"W={world} {case}")
 
 
 def test_gpu_shard_c4_shape(rccl_solver, twin):
@@ -84,15 +87,15 @@ def test_gpu_shard_c4_shape(rccl_solver, twin):
     assert_same_as_single(r, twin.solve(a), "C4")
 
 
-def test_gpu_shard_c4_world8(twin):
+def test_gpu_shard_c4_world8(shard_lib):
     c = ss.C4
     a = ss.synth_problem(12, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
     r = gpu_shard_threads(a, 8)
-    assert_same_as_single(r, twin.solve(a), "C4 W=8")
+    assert_same_as_single(r, run_threads(shard_lib, a, 8), "C4 W=8")
 
 
 @pytest.mark.parametrize("world", [2])
-def test_gpu_shard_peer_transport_threaded_ranks(world, twin):
+def test_gpu_shard_peer_transport_threaded_ranks(world, shard_lib):
     """sw_dist_enable_peer with ranks that are threads of ONE process,
     entering the setup concurrently: every rank must see the same process
     identity (one nonce per process, initialised once) and take the
@@ -107,7 +110,7 @@ def test_gpu_shard_peer_transport_threaded_ranks(world, twin):
         a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
         r = gpu_shard_threads(a, world, peer=True)
         check_plan_valid(a, r)
-        assert_same_as_single(r, twin.solve(a), f"peer threads W={world} {case}")
+        assert_same_as_single(r, run_threads(shard_lib, a, world), f"peer threads W={world} {case}")
 
 
 def test_gpu_shard_rejects_bad_slice(rccl_solver):
@@ -148,11 +151,11 @@ def test_gpu_shard_device_rejects_bad_input(rccl_solver):
     assert r["rc"] in (0, 1)
 
 
-def test_gpu_shard_peer_transport_two_processes(tmp_path, twin):
+def test_gpu_shard_peer_transport_two_processes(tmp_path, shard_lib):
     """sw_dist_enable_peer: two processes on cuda:0 (gloo only for the setup),
     every step's all-reduce / all-gather one k_xchg kernel writing into the
-    other process's IPC-mapped exchange region; the result must be the
-    single-instance twin's, bit for bit, C4 shape included."""
+    other process's IPC-mapped exchange region; the result must be the CPU
+    shard engine's at world 2, bit for bit, C4 shape included."""
     import json
     import os
     import socket
@@ -190,7 +193,7 @@ def test_gpu_shard_peer_transport_two_processes(tmp_path, twin):
             parts.append((int(z["lo"]), int(z["hi"]), res))
         rs = assemble(a, parts)
         check_plan_valid(a, rs)
-        assert_same_as_single(rs, twin.solve(a), f"peer W=2 {case}")
+        assert_same_as_single(rs, run_threads(shard_lib, a, 2), f"peer W=2 {case}")
 
 
 def test_gpu_shard_peer_late_rank_fails_cleanly(tmp_path):
@@ -238,16 +241,17 @@ def test_gpu_shard_fuzz_rccl_world1(rccl_solver, twin):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_gpu_shard_fuzz_host_comm(world, twin):
+def test_gpu_shard_fuzz_host_comm(world, shard_lib):
     from fuzzcases import fuzz_problem
 
     for s in range(256, 256 + 48):
         a = fuzz_problem(s)
-        assert_same_as_single(gpu_shard_threads(a, world), twin.solve(a), f"W={world} fuzz seed {s}")
+        assert_same_as_single(gpu_shard_threads(a, world), run_threads(shard_lib, a, world),
+                              f"W={world} fuzz seed {s}")
 
 
 @pytest.mark.parametrize("world", [1, 2])
-def test_gpu_shard_pattern_placement(world, rccl_solver, twin):
+def test_gpu_shard_pattern_placement(world, rccl_solver, twin, shard_lib):
     """The level search's branch and bound and the round-pattern placement on
     the GPU engine (frag-fuzz seeds of tests/test_shard.py): RCCL at world 1,
     host collectives at world 2, each equal to the twin bit for bit."""
@@ -261,10 +265,11 @@ def test_gpu_shard_pattern_placement(world, rccl_solver, twin):
         a = mk.instance(s)
         r = rccl_solver.dist_solve(a, 0, a.N) if world == 1 else gpu_shard_threads(a, world)
         check_plan_valid(a, r)
-        assert_same_as_single(r, twin.solve(a), f"W={world} frag seed {s}")
+        ref = twin.solve(a) if world == 1 else run_threads(shard_lib, a, world)
+        assert_same_as_single(r, ref, f"W={world} frag seed {s}")
 
 
-def test_gpu_shard_peer_refuses_too_many_same_device_ranks(twin):
+def test_gpu_shard_peer_refuses_too_many_same_device_ranks(shard_lib):
     """Four ranks of one process on one device exceed half of the process's
     hardware queues (GPU_MAX_HW_QUEUES = 4 on the box): sw_dist_enable_peer
     refuses on every rank with SW_ERR_INVALID at once (no 10 s timeout), and
@@ -306,4 +311,30 @@ def test_gpu_shard_peer_refuses_too_many_same_device_ranks(twin):
     assert not errs, errs
     assert codes == [sn.SW_ERR_INVALID] * world, codes
     assert time.time() - t0 < 60
-    assert_same_as_single(assemble(a, out), twin.solve(a), "after the refusal")
+    assert_same_as_single(assemble(a, out), run_threads(shard_lib, a, world), "after the refusal")
+
+
+def test_gpu_workspace_resolve_paths_match_twin(rccl_solver, twin, shard_lib):
+    """Re-solved (SW_STATUS_P1_REPACKED) instances above 1,024 jobs: the plan
+    kernel's workspace form (per-round re-optimisation with its items in the
+    position slots and values in workspace rows; the pattern search's scratch
+    in LDS at 1,500 jobs, in the workspace rows at 2,000) through
+    sw_plan_solve, and the sharded engines' gathered k_rr at world 1 (RCCL)
+    and 2 (host collectives): equal to the twin (world 1) or the CPU shard
+    engine (world 2) bit for bit."""
+    cases = [(0, 1500), (2, 1500), (3, 1500), (3, 2000)]
+    rep = 0
+    s = sn.Solver(device=0)
+    for seed, N in cases:
+        a = ss.synth_problem(seed, N, 12, 12, 120.0, 1.0, 5.0, width_p=(0.4, 0.3, 0.2, 0.1))
+        rt = twin.solve(a)
+        rep += bool(rt["status"] & sn.SW_STATUS_P1_REPACKED)
+        r1 = s.solve(a)
+        check_plan_valid(a, r1)
+        assert_same_as_single(r1, rt, f"sw_plan_solve seed {seed} N {N}")
+        assert r1["iters"] == rt["iters"]
+        assert_same_as_single(rccl_solver.dist_solve(a, 0, a.N), rt, f"dist W=1 seed {seed} N {N}")
+        assert_same_as_single(gpu_shard_threads(a, 2), run_threads(shard_lib, a, 2),
+                              f"dist W=2 seed {seed} N {N}")
+    s.close()
+    assert rep >= 2, rep

@@ -3,10 +3,19 @@
 The controller (csrc/sw_shard_ctl.h) runs here on the CPU shard engine
 (oracle/shard_twin.c) with W ranks as threads (a barrier-based allgather) and,
 for the multi-process path, as W=2 processes over torch.distributed gloo.
-The bar: for every world size W | 512 the sharded solve returns exactly the
-single-instance result of the twin (oracle/plan_twin.c), which the GPU kernel
-matches bit for bit (tests/test_gpu_parity.py) — plan rows, counts and the
-bits of every objective.  Only `iters` differs (it counts collective steps).
+
+The contract.  The CPU shard engine is the specification the
+GPU engine (csrc/sw_shard.hip) matches bit for bit at every world size
+(tests/test_gpu_shard.py).  Against the single-instance solve (the twin,
+oracle/plan_twin.c, = the GPU plan kernel):
+  * W = 1: the same result, bit for bit (plan rows, counts, every objective);
+  * W > 1: every rank places its own jobs in its share of each round (the
+    share placement, sw_share_caps), so the plan rows and the P2 objective
+    depend on W; P1 — counts, objective, utility, makespan, bound and the P1
+    status bits — is the single-instance solve's bit for bit (the same level
+    search, every count placed), or better when only the shares could place
+    the level search's counts; P2 stays within SHARE_P2_RATIO of the single
+    instance's.  Only `iters` differs at every W (it counts collective steps).
 """
 import ctypes
 import os
@@ -100,6 +109,35 @@ def assemble(a, parts):
     return dict(r0, plan=plan, planned_rounds=cnt)
 
 
+P1_BITS = sn.SW_STATUS_P1_REPACKED | sn.SW_STATUS_NO_PLANNED | sn.SW_STATUS_P1_UNCERTIFIED
+# the share placement's P2 against the single instance's (both after the
+# exchange step): ≤ 1.002 measured over these cases, the fuzz set and C4
+SHARE_P2_RATIO = 1.005
+
+
+def assert_share_contract(rs, rt, what):
+    """W > 1 against the single-instance result rt (the module docstring)."""
+    assert rs["rc"] >= 0, what
+    if (rs["status"] & P1_BITS) == (rt["status"] & P1_BITS):
+        assert np.array_equal(rs["planned_rounds"], rt["planned_rounds"]), f"{what}: counts"
+        for key in ("objective", "utility", "makespan", "bound"):
+            assert np.float64(rs[key]).tobytes() == np.float64(rt[key]).tobytes(), \
+                f"{what}: {key} {rs[key]!r} vs {rt[key]!r}"
+        if rt["p2_objective"] > 0:
+            assert rs["p2_objective"] <= rt["p2_objective"] * SHARE_P2_RATIO, \
+                (what, rs["p2_objective"], rt["p2_objective"])
+    else:  # the shares placed the level search's counts, the gathered orders could not
+        assert rt["status"] & sn.SW_STATUS_P1_REPACKED and not rs["status"] & sn.SW_STATUS_P1_REPACKED, what
+        assert rs["objective"] >= rt["objective"], what
+
+
+def assert_contract(rs, rt, world, what):
+    if world == 1:
+        assert_same_as_single(rs, rt, what)
+    else:
+        assert_share_contract(rs, rt, what)
+
+
 def assert_same_as_single(rs, rt, what):
     assert rs["status"] == rt["status"], what
     assert rs["rc"] == rt["rc"], what
@@ -127,13 +165,13 @@ CASES = [
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 @pytest.mark.parametrize("case", CASES, ids=[f"N{c[1]}_G{c[2]}_T{c[3]}_k{c[4]:g}" for c in CASES])
-def test_sharded_equals_single(case, world, shard_lib, twin):
+def test_sharded_vs_single(case, world, shard_lib, twin):
     seed, N, G, T, k, lam = case
     a = ss.synth_problem(seed, N, G, T, 120.0, k, lam)
     rs = run_threads(shard_lib, a, world)
     rt = twin.solve(a)
     check_plan_valid(a, rs)
-    assert_same_as_single(rs, rt, f"W={world} case {case}")
+    assert_contract(rs, rt, world, f"W={world} case {case}")
 
 
 def test_sharded_edge_cases(shard_lib, twin):
@@ -143,13 +181,13 @@ def test_sharded_edge_cases(shard_lib, twin):
     assert rs["status"] & sn.SW_STATUS_NO_PLANNED
     a = ss.synth_problem(2, 64, 4, 10, 120.0, 1e2, 5.0)
     a.w[::3] = 8  # wider than G=4: never schedulable
-    assert_same_as_single(run_threads(shard_lib, a, 4), twin.solve(a), "wide jobs")
+    assert_share_contract(run_threads(shard_lib, a, 4), twin.solve(a), "wide jobs")
     a1 = ss.synth_problem(3, 1, 8, 5, 120.0, 1e5, 5.0)
-    assert_same_as_single(run_threads(shard_lib, a1, 8), twin.solve(a1), "one job")
+    assert_share_contract(run_threads(shard_lib, a1, 8), twin.solve(a1), "one job")
     at = ss.synth_problem(4, 96, 16, 8, 120.0, 1e1, 5.0)
     for arr in (at.w, at.d, at.F, at.E, at.R, at.p):
         arr[:] = arr[0]
-    assert_same_as_single(run_threads(shard_lib, at, 4), twin.solve(at), "ties")
+    assert_share_contract(run_threads(shard_lib, at, 4), twin.solve(at), "ties")
 
 
 def test_shard_range_rule():
@@ -200,7 +238,7 @@ def _gloo_worker(rank, world, port, outdir, cases):
     dist.destroy_process_group()
 
 
-def test_sharded_gloo_world2(tmp_path, twin):
+def test_sharded_gloo_world2(tmp_path, shard_lib, twin):
     import socket
 
     import torch.multiprocessing as mp
@@ -221,11 +259,13 @@ def test_sharded_gloo_world2(tmp_path, twin):
                        plan=z["plan"], planned_rounds=z["cnt"])
             parts.append((int(z["lo"]), int(z["hi"]), res))
         rs = assemble(a, parts)
-        assert_same_as_single(rs, twin.solve(a), f"gloo case {case}")
+        # processes over gloo = threads in one process: the same engine, bit for bit
+        assert_same_as_single(rs, run_threads(shard_lib, a, 2), f"gloo case {case}")
+        assert_share_contract(rs, twin.solve(a), f"gloo case {case}")
 
 
 @pytest.mark.parametrize("world", [1, 2, 4])
-def test_sharded_fuzz_equals_single(world, shard_lib, twin):
+def test_sharded_fuzz_vs_single(world, shard_lib, twin):
     """The fuzz instances of tests/fuzzcases.py (validator-range inputs, exact
     duplicate jobs, finished jobs, zero priorities, custom base grids)."""
     from fuzzcases import fuzz_problem
@@ -234,7 +274,7 @@ def test_sharded_fuzz_equals_single(world, shard_lib, twin):
         a = fuzz_problem(s)
         rs = run_threads(shard_lib, a, world)
         check_plan_valid(a, rs)
-        assert_same_as_single(rs, twin.solve(a), f"W={world} fuzz seed {s}")
+        assert_contract(rs, twin.solve(a), world, f"W={world} fuzz seed {s}")
 
 
 @pytest.mark.parametrize("world", [1, 2, 4])
@@ -254,6 +294,6 @@ def test_sharded_pattern_placement_equals_single(world, shard_lib, twin):
         rs = run_threads(shard_lib, a, world)
         check_plan_valid(a, rs)
         rt = twin.solve(a)
-        assert_same_as_single(rs, rt, f"W={world} frag seed {s}")
+        assert_contract(rs, rt, world, f"W={world} frag seed {s}")
         if s == 50115:
             assert not rt["status"] & sn.SW_STATUS_P1_REPACKED  # placed as counted
