@@ -297,3 +297,23 @@ def test_sharded_pattern_placement_equals_single(world, shard_lib, twin):
         assert_contract(rs, rt, world, f"W={world} frag seed {s}")
         if s == 50115:
             assert not rt["status"] & sn.SW_STATUS_P1_REPACKED  # placed as counted
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_share_p2_vs_milp_on_large_instances(world, shard_lib, twin):
+    """The share placement's P2 at 3,000 and 5,000 jobs (C4-shaped) against
+    the HiGHS optimum of the reference P2 MILP on the same counts
+    (tests/golden/p2_share.json): the counts are the single instance's, and
+    the P2 objective stays within SHARE_P2_RATIO of the optimum."""
+    import json
+
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                       "p2_share.json")))["cases"]
+    for c in gold:
+        a = ss.synth_problem(c["seed"], c["N"], c["G"], c["T"], 120.0, c["k"], c["lam"])
+        rs = run_threads(shard_lib, a, world)
+        check_plan_valid(a, rs)
+        assert np.array_equal(rs["planned_rounds"], np.asarray(c["counts"], np.int32))
+        assert rs["p2_objective"] <= c["p2_milp"] * SHARE_P2_RATIO, \
+            (c["N"], world, rs["p2_objective"] / c["p2_milp"])
+        assert_share_contract(rs, twin.solve(a), f"N={c['N']} W={world}")
