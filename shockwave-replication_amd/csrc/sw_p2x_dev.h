@@ -39,6 +39,25 @@ struct sw_p2x_arrays {
 static_assert(SW_P2X_ARR_BYTES == 2 * sizeof(int32_t) + sizeof(double) + sizeof(uint64_t),
               "SW_P2X_ARR_BYTES (sw_p2x.h) must cover the sw_p2x_arrays layout");
 
+/* The step's set-up, prepared in HBM by several workgroups (the sharded
+ * engine's k_p2x_pre*, sw_shard.hip) instead of by the step's one workgroup:
+ * the classes (hdr: K, wc[8], M[8], off[9], nw[8], boff[8]), the positions'
+ * active indices and c (ord, pc), the rank bitsets B (the layout of LDS
+ * below) and, per load size index ki, the first edge-cost matrix (Wb: the
+ * cheapest class's cost without δ, SW_P2X_NONE for none; Wk: its class) —
+ * what sw_p2x_block would compute, the same values.  The matrices serve the
+ * first build of each load size while nothing was cancelled. */
+struct sw_p2x_pre {
+    const int32_t* hdr;
+    const int32_t* ord;
+    const double* pc;
+    const uint64_t* B;
+    const double* Wb;
+    const int8_t* Wk;
+};
+enum { SW_P2X_HDR_K = 0, SW_P2X_HDR_WC = 1, SW_P2X_HDR_M = 9, SW_P2X_HDR_OFF = 17,
+       SW_P2X_HDR_NW = 26, SW_P2X_HDR_BOFF = 34, SW_P2X_HDR_A = 42, SW_P2X_HDR_INTS = 48 };
+
 /* fixed LDS part */
 struct sw_p2x_lds {
     sw_xchg X;
@@ -452,7 +471,7 @@ static __device__ __forceinline__ void p2x_sort_regs(uint64_t (&hi)[EMAX], uint6
 template <int NW, int EMAX = 1>
 __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, unsigned char* var,
                                             const sw_p2x_arrays& X, int A, int T, int G,
-                                            uint64_t* sp = nullptr) {
+                                            uint64_t* sp = nullptr, const sw_p2x_pre* pre = nullptr) {
     constexpr int NT = NW * 64;
     const int tid = threadIdx.x;
     (void)sp;
@@ -461,6 +480,19 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     uint64_t sp_t_ = __builtin_amdgcn_s_memtime();
 #endif
     if (A <= 0 || T < 2 || A > SW_P2X_AMAX) return 0;
+    if (pre && pre->hdr[SW_P2X_HDR_K] < 0) return 0; /* more than SW_P2X_KMAX classes */
+    if (pre) { /* the prepared set-up: classes, positions, bitsets from HBM */
+        if (tid < SW_P2X_KMAX) {
+            L->wc[tid] = pre->hdr[SW_P2X_HDR_WC + tid];
+            L->M[tid] = pre->hdr[SW_P2X_HDR_M + tid];
+            L->nw[tid] = pre->hdr[SW_P2X_HDR_NW + tid];
+            L->boff[tid] = pre->hdr[SW_P2X_HDR_BOFF + tid];
+        }
+        if (tid <= SW_P2X_KMAX) L->off[tid] = pre->hdr[SW_P2X_HDR_OFF + tid];
+        if (tid == 0) L->K = pre->hdr[SW_P2X_HDR_K];
+        __syncthreads();
+    }
+    if (!pre) {
     /* ---- width classes (ascending) ---- */
     if (tid < 8) L->wmap[tid] = 0u;
     __syncthreads();
@@ -480,11 +512,11 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
         }
     }
     __syncthreads();
-    const int K = L->K;
-    if (K < 0) return 0;
+    if (L->K < 0) return 0;
     for (int a = tid; a < A; a += NT) atomicAdd(&L->M[p2x_class(L, X.cw[a])], 1);
     __syncthreads();
     if (tid == 0) {
+        const int K = L->K;
         int o = 0, b = 0;
         for (int k = 0; k < K; ++k) {
             L->off[k] = o;
@@ -495,6 +527,8 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
         }
         L->off[K] = o;
     }
+    } /* !pre */
+    const int K = L->K;
     P2X_STAMP(0);
     /* LDS carve-up of var */
     double* pc = reinterpret_cast<double*>(var);                      /* c by position        */
@@ -509,7 +543,14 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
     /* ---- positions: (class asc, sw_p2x_ckey(c) desc, job asc) by a bitonic
      *      sort in LDS over the next power of two (the bitset / W area is
      *      free until the first build) ---- */
-    if (A <= NT) {
+    if (pre) {
+        for (int p = tid; p < A; p += NT) {
+            ord[p] = pre->ord[p];
+            pc[p] = pre->pc[p];
+        }
+        for (int i = tid; i < nwords; i += NT) B[i] = pre->B[i];
+        __syncthreads();
+    } else if (A <= NT) {
         /* one position per thread: (class, key) and (job << 32 | a), a
          * bitonic network over the next power of two np with shuffles for
          * strides < 64 and an LDS exchange above (16·np bytes, what the
@@ -647,6 +688,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
         const int lane = lane_id(), wv = wave_id();
         int nslot = 0;
         for (int k = 0; k < K; ++k) nslot += L->nw[k];
+        if (pre) nslot = 0; /* the bitsets came prepared */
         for (int sl = wv; sl < nslot; sl += NW) {
             int k = 0, w = sl;
             while (w >= L->nw[k]) w -= L->nw[k++];
@@ -711,7 +753,17 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
             __syncthreads();
             bool all = true;
             while (ncancel < SW_P2X_MAX_CANCEL) {
-                p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
+                if (pre && all && ncancel == 0) { /* the prepared first build of this load size */
+                    const double* Wb = pre->Wb + (size_t)ki * T * T;
+                    const int8_t* Wkb = pre->Wk + (size_t)ki * T * T;
+                    for (int e = tid; e < T * T; e += NT) {
+                        const double b = Wb[e];
+                        W[e] = b < SW_P2X_NONE ? b + delta : SW_P2X_NONE;
+                        Wk[e] = Wkb[e];
+                    }
+                } else {
+                    p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
+                }
                 __syncthreads();
                 P2X_STAMP(3);
                 sp_a_[8] += 1;

@@ -102,10 +102,28 @@ struct sw_pack_lds {
  */
 /* Room after round t for jobs with more than m rounds left, lane m:
  * the R−1−m smallest capacities of rounds t+1 … T−1 (twin: Lsum[R−1−m]);
- * G·(R−1−m) when every round has capacity G (caps == nullptr). */
-__device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int R, int G) {
+ * G·(R−1−m) when every round has capacity G (caps == nullptr).  cbase ≥ 0:
+ * every capacity is cbase or cbase + 1 (the share placement's shares,
+ * sw_share_caps): the x smallest of the later rounds then sum to
+ * x·cbase + max(0, x − #{later rounds at cbase}), one ballot instead of a
+ * wave sort — the same value. */
+__device__ __forceinline__ int32_t sw_pack_caps_base(const int32_t* caps, int T) {
+    if (!caps) return -1;
+    const int lane = lane_id();
+    const int32_t mn = wave_min_i32(lane < T ? caps[lane] : 0x7FFFFFFF);
+    const int32_t mx = wave_max_i32(lane < T ? caps[lane] : (int32_t)0x80000000);
+    return mx - mn <= 1 ? mn : -1;
+}
+
+__device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int R, int G,
+                                                int32_t cbase = -1) {
     const int lane = lane_id();
     if (!caps) return G * (R - 1 - lane);
+    if (cbase >= 0) {
+        const int32_t nb = __popcll(__ballot(lane < R - 1 && caps[t + 1 + lane] == cbase));
+        const int32_t x = R - 1 - lane;
+        return x > 0 ? x * cbase + (x > nb ? x - nb : 0) : 0;
+    }
     int32_t v = (lane < R - 1) ? caps[t + 1 + lane] : 0x7FFFFFFF;
     v = wave_sort_asc_i32(v);
     v = (lane < R - 1) ? v : 0;
@@ -132,6 +150,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
     if (tid < 68) Hu[tid] = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) mk[i] = 0;
+    const int32_t cbase = sw_pack_caps_base(caps, T);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < E; ++i)
@@ -150,7 +169,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
         /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-        const int32_t room = sw_pack_room(caps, t, R, G);
+        const int32_t room = sw_pack_room(caps, t, R, G, cbase);
         const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
         SWP_STAMP(1);
         /* tiers: jobs with more than m rounds left must shed enough now */
@@ -291,6 +310,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
 #pragma unroll
     for (int i = 0; i < E1; ++i)
         if (st[i] != 0u) atomicAdd(&Hm[RR_(i)], WW_(i));
+    const int32_t cbase = sw_pack_caps_base(caps, T);
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
@@ -310,7 +330,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
         const int32_t hv = (lane + 1 < R) ? h1 : (lane + 1 == R ? tailR : 0);
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-        const int32_t room = sw_pack_room(caps, t, R, G);
+        const int32_t room = sw_pack_room(caps, t, R, G, cbase);
         const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
         SWP_STAMP(1);
         int mstart = R - 1;

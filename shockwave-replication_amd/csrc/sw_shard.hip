@@ -862,11 +862,171 @@ __global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, 
     out[i] = e;
 }
 
+/* ---- the step's set-up by several workgroups (sw_p2x_pre, sw_p2x_dev.h):
+ * the single-workgroup step then starts from the prepared classes,
+ * positions, bitsets and first edge costs instead of building them itself
+ * (C4: a 4,096-entry rank sort and four full edge builds in one workgroup,
+ * ~190 of its ~225 µs).  Same values, so the same result bit for bit. */
+
+/* one workgroup: the active entries compacted in job order into the X
+ * arrays (as k_p2x does), their width classes (hdr) and the rank-sort keys
+ * (class asc, sw_p2x_ckey(c) desc, job asc, as descending (~hi, ~lo) keys
+ * for k_pack_chunk_sort; entry a of keys = active entry a) */
+__global__ __launch_bounds__(SW_BLOCK) void k_p2x_pre0(const p2x_ent* all, int64_t M, int T,
+                                                       unsigned char* ws, int32_t* hdr,
+                                                       sw_pack_ent* keys) {
+    __shared__ sw_xchg Xc;
+    __shared__ uint32_t wmap[8];
+    __shared__ int32_t cls[SW_P2X_KMAX], cnt[SW_P2X_KMAX];
+    __shared__ int32_t Ks;
+    sw_blk blk;
+    blk.X = &Xc;
+    blk.par = 0;
+    sw_p2x_arrays X;
+    X.cc = reinterpret_cast<double*>(ws);
+    X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
+    X.cw = reinterpret_cast<int32_t*>(X.cm + M);
+    X.cj = X.cw + M;
+    const int tid = threadIdx.x;
+    const int64_t q = (M + SW_BLOCK - 1) / SW_BLOCK;
+    const int64_t j0 = (int64_t)tid * q, j1 = j0 + q < M ? j0 + q : M;
+    int act = 0;
+    for (int64_t j = j0; j < j1; ++j) act += all[j].n > 0;
+    if (tid < 8) wmap[tid] = 0u;
+    if (tid < SW_P2X_KMAX) cnt[tid] = 0;
+    int A;
+    int a = blk.exscan(act, A); /* its barrier publishes wmap, cnt */
+    for (int64_t j = j0; j < j1; ++j) {
+        const p2x_ent e = all[j];
+        if (e.n <= 0) continue;
+        X.cw[a] = e.w;
+        X.cj[a] = (int32_t)j;
+        X.cc[a] = e.p / (double)e.n;
+        X.cm[a] = e.m;
+        atomicOr(&wmap[(e.w >> 5) & 7], 1u << (e.w & 31));
+        ++a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int K = 0;
+        for (int i = 0; i < 8; ++i) K += __builtin_popcount(wmap[i]);
+        if (K > SW_P2X_KMAX) {
+            K = -1;
+        } else {
+            K = 0;
+            for (int i = 0; i < 8; ++i)
+                for (uint32_t b = wmap[i]; b; b &= b - 1) cls[K++] = 32 * i + __builtin_ctz(b);
+        }
+        Ks = K;
+    }
+    __syncthreads();
+    const int K = Ks;
+    if (K >= 0)
+        for (int i = tid; i < A; i += SW_BLOCK) {
+            int k = 0;
+            while (k < K - 1 && cls[k] != X.cw[i]) ++k;
+            atomicAdd(&cnt[k], 1);
+            const uint64_t ck = sw_p2x_ckey(X.cc[i]);
+            const uint64_t hi = ((uint64_t)k << 61) | (~ck & ((1ull << 61) - 1));
+            const uint64_t lo = ((uint64_t)(uint32_t)X.cj[i] << 32) | (uint32_t)i;
+            sw_pack_ent e;
+            e.khi = ~hi;
+            e.klo = ~lo;
+            e.st = 1u;
+            e.pad = 0u;
+            keys[i] = e;
+        }
+    for (int64_t i = (int64_t)A + tid; i < M; i += SW_BLOCK) {
+        sw_pack_ent e;
+        e.khi = 0; e.klo = 0; e.st = 0u; e.pad = 0u;
+        keys[i] = e;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        hdr[SW_P2X_HDR_K] = K;
+        hdr[SW_P2X_HDR_A] = A;
+        int o = 0, b = 0;
+        for (int k = 0; k < SW_P2X_KMAX; ++k) {
+            const int m = (K >= 0 && k < K) ? cnt[k] : 0;
+            hdr[SW_P2X_HDR_WC + k] = (K >= 0 && k < K) ? cls[k] : 0;
+            hdr[SW_P2X_HDR_M + k] = m;
+            hdr[SW_P2X_HDR_OFF + k] = o;
+            hdr[SW_P2X_HDR_NW + k] = (m + 63) / 64;
+            hdr[SW_P2X_HDR_BOFF + k] = b;
+            o += m;
+            b += ((m + 63) / 64) * T; /* word offsets, as sw_p2x_block's boff */
+        }
+        hdr[SW_P2X_HDR_OFF + SW_P2X_KMAX] = o;
+    }
+}
+
+/* positions and bitsets: one wave per 64-rank word slot (class k, word w):
+ * lane r takes position off[k] + 64·w + r (ord, pc) and each round's word is
+ * one ballot (the layout of sw_p2x_block: word w of round t at boff[k]·T +
+ * w·T + t) */
+__global__ __launch_bounds__(kTB) void k_p2x_pre_bits(const int32_t* hdr, const int32_t* order,
+                                                      const unsigned char* ws, int64_t M, int T,
+                                                      int32_t* ord, double* pc, uint64_t* B) {
+    const int K = hdr[SW_P2X_HDR_K];
+    if (K <= 0) return;
+    const double* cc = reinterpret_cast<const double*>(ws);
+    const uint64_t* cm = reinterpret_cast<const uint64_t*>(cc + M);
+    const int lane = lane_id();
+    int sl = (int)((blockIdx.x * kTB + threadIdx.x) >> 6);
+    int k = 0;
+    while (k < K && sl >= hdr[SW_P2X_HDR_NW + k]) sl -= hdr[SW_P2X_HDR_NW + k++];
+    if (k >= K) return;
+    const int r = 64 * sl + lane;
+    const int p = hdr[SW_P2X_HDR_OFF + k] + r;
+    uint64_t m = 0;
+    if (r < hdr[SW_P2X_HDR_M + k]) {
+        const int a = order[p];
+        ord[p] = a;
+        pc[p] = cc[a];
+        m = cm[a];
+    }
+    uint64_t* Bk = B + (size_t)hdr[SW_P2X_HDR_BOFF + k] + (size_t)sl * T;
+    for (int t = 0; t < T; ++t) {
+        const uint64_t word = __ballot((m >> t) & 1ull);
+        if (lane == 0) Bk[t] = word;
+    }
+}
+
+/* the first edge costs of every load size F (each class width): entry
+ * (ki, t, u), the cheapest class k with w_k | F, F / w_k ≤ SW_P2X_QMAX
+ * (ascending k on ties), without δ — oracle/p2x_twin.c build_w */
+__global__ __launch_bounds__(kTB) void k_p2x_pre_w(const int32_t* hdr, const double* pc,
+                                                   const uint64_t* B, int T, double* Wb, int8_t* Wk) {
+    const int K = hdr[SW_P2X_HDR_K];
+    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (K <= 0 || e >= (int64_t)K * T * T) return;
+    const int ki = (int)(e / (T * T)), tu = (int)(e % (T * T)), t = tu / T, u = tu % T;
+    const int F = hdr[SW_P2X_HDR_WC + ki];
+    double best = SW_P2X_NONE;
+    int bk = -1;
+    if (t != u)
+        for (int k = 0; k < K; ++k) {
+            const int wk = hdr[SW_P2X_HDR_WC + k];
+            if (wk > F || F % wk != 0 || F / wk > SW_P2X_QMAX) continue;
+            const uint64_t* Bk = B + (size_t)hdr[SW_P2X_HDR_BOFF + k];
+            const double cost = sw_p2x_cost(Bk + t, Bk + u, hdr[SW_P2X_HDR_NW + k], T, F / wk, t, u,
+                                            pc + hdr[SW_P2X_HDR_OFF + k]);
+            if (cost < best) {
+                best = cost;
+                bk = k;
+            }
+        }
+    Wb[e] = best;
+    Wk[e] = (int8_t)bk;
+}
+
 /* The step on the M gathered entries (entry j = job j), one workgroup, the
  * same on every rank; writes this rank's rows of ydst and the number of
- * cycles cancelled into red[0]. */
+ * cycles cancelled into red[0].  pre: the prepared set-up (k_p2x_pre*; the
+ * X arrays are then already compacted in ws). */
 __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all, int64_t M,
-                                                  unsigned char* ws, uint64_t* ydst) {
+                                                  unsigned char* ws, uint64_t* ydst, sw_p2x_pre pre,
+                                                  int prepared) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     sw_p2x_lds* L = reinterpret_cast<sw_p2x_lds*>(smem);
     unsigned char* var = smem + ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15);
@@ -878,23 +1038,28 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all
     X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
     X.cw = reinterpret_cast<int32_t*>(X.cm + M);
     X.cj = X.cw + M;
-    const int64_t q = (M + SW_BLOCK - 1) / SW_BLOCK;
-    const int64_t j0 = (int64_t)threadIdx.x * q, j1 = j0 + q < M ? j0 + q : M;
-    int act = 0;
-    for (int64_t j = j0; j < j1; ++j) act += all[j].n > 0;
     int A;
-    int a = blk.exscan(act, A);
-    for (int64_t j = j0; j < j1; ++j) {
-        const p2x_ent e = all[j];
-        if (e.n <= 0) continue;
-        X.cw[a] = e.w;
-        X.cj[a] = (int32_t)j;
-        X.cc[a] = e.p / (double)e.n;
-        X.cm[a] = e.m;
-        ++a;
+    if (prepared) {
+        A = pre.hdr[SW_P2X_HDR_A];
+    } else {
+        const int64_t q = (M + SW_BLOCK - 1) / SW_BLOCK;
+        const int64_t j0 = (int64_t)threadIdx.x * q, j1 = j0 + q < M ? j0 + q : M;
+        int act = 0;
+        for (int64_t j = j0; j < j1; ++j) act += all[j].n > 0;
+        int a = blk.exscan(act, A);
+        for (int64_t j = j0; j < j1; ++j) {
+            const p2x_ent e = all[j];
+            if (e.n <= 0) continue;
+            X.cw[a] = e.w;
+            X.cj[a] = (int32_t)j;
+            X.cc[a] = e.p / (double)e.n;
+            X.cm[a] = e.m;
+            ++a;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    const int nc = sw_p2x_block<SW_WAVES, 8>(blk, L, var, X, A, S.T, S.G);
+    const int nc = sw_p2x_block<SW_WAVES, 8>(blk, L, var, X, A, S.T, S.G, nullptr,
+                                             prepared ? &pre : nullptr);
     if (nc > 0)
         for (int i = threadIdx.x; i < A; i += SW_BLOCK) {
             const int64_t j = X.cj[i];
@@ -1215,7 +1380,8 @@ struct sw_shard_state {
     DevBuf<uint8_t> plan;
     DevBuf<long long> red, tieblk;
     DevBuf<sw_pack_ent> pall;
-    DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry) */
+    DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry), prepared set-up */
+    DevBuf<sw_pack_ent> p2keys; /* the exchange's rank-sort keys (k_p2x_pre0) */
     DevBuf<unsigned char> rrin, rrrow, rrws; /* re-optimisation: gathered entries, workspace */
     DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
@@ -1831,8 +1997,49 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
     SH_TRY(zero_red(S, 1));
     const int maxA = (int)std::min<int64_t>(M, SW_P2X_AMAX);
     const size_t lds = ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15) + sw_p2x_var_bytes(maxA, S->T);
+    /* the set-up by several workgroups (k_p2x_pre*) when the gathered entries
+     * fill more than one workgroup's sort: the step's own workgroup then
+     * starts from the prepared state */
+    sw_p2x_pre pre;
+    memset(&pre, 0, sizeof(pre));
+    const int T = S->T;
+    const bool prepared = M > SW_BLOCK && M <= SW_P2X_AMAX * 4;
+    if (prepared) {
+        /* workspace after the X arrays: hdr, ord, pc, bitsets, Wb, Wk */
+        const size_t xa = ((size_t)M * SW_P2X_ARR_BYTES + 15) & ~(size_t)15;
+        const size_t words = (size_t)T * ((size_t)(M + 63) / 64 + SW_P2X_KMAX);
+        const size_t need = xa + 256 + (size_t)M * 4 + (size_t)M * 8 + words * 8 +
+                            (size_t)SW_P2X_KMAX * T * T * 9 + 64;
+        if (S->p2ws.reserve(need) || S->p2keys.reserve((size_t)M))
+            return host_fail(S, "P2 exchange workspace");
+        unsigned char* base = S->p2ws.p + xa;
+        int32_t* hdr = reinterpret_cast<int32_t*>(base);
+        int32_t* ord = reinterpret_cast<int32_t*>(base + 256);
+        double* pc = reinterpret_cast<double*>(base + 256 + (((size_t)M * 4 + 15) & ~(size_t)15));
+        uint64_t* B = reinterpret_cast<uint64_t*>(pc + M);
+        double* Wb = reinterpret_cast<double*>(B + words);
+        int8_t* Wk = reinterpret_cast<int8_t*>(Wb + (size_t)SW_P2X_KMAX * T * T);
+        LAUNCH(S, k_p2x_pre0, dim3(1), dim3(SW_BLOCK), 0, st, (const p2x_ent*)gv, M, T, S->p2ws.p, hdr,
+               S->p2keys.p);
+        const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
+        LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, S->p2keys.p, M, S->skeys.p,
+               S->sidx.p);
+        LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
+               S->sidx.p, nch, S->porder.p);
+        const int64_t slots = (M + 63) / 64 + SW_P2X_KMAX;
+        LAUNCH(S, k_p2x_pre_bits, dim3(nblk(slots * 64)), dim3(kTB), 0, st, hdr, S->porder.p, S->p2ws.p,
+               M, T, ord, pc, B);
+        LAUNCH(S, k_p2x_pre_w, dim3(nblk((int64_t)SW_P2X_KMAX * T * T)), dim3(kTB), 0, st, hdr, pc, B, T,
+               Wb, Wk);
+        pre.hdr = hdr;
+        pre.ord = ord;
+        pre.pc = pc;
+        pre.B = B;
+        pre.Wb = Wb;
+        pre.Wk = Wk;
+    }
     LAUNCH(S, k_p2x, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, (const p2x_ent*)gv, M, S->p2ws.p,
-           S->y[ysrc].p);
+           S->y[ysrc].p, pre, (int)prepared);
     uint64_t nc = 0;
     SH_TRY(coll_reduce(S, S->dv.red, 1, 1, &nc)); /* every rank computed the same count */
     *cancels = (int32_t)nc;
@@ -1978,6 +2185,7 @@ void sw_shard_release(sw_handle* h) {
     if (S->pub) (void)hipHostFree(S->pub);
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
+    S->p2keys.release();
     S->caps.release(); S->hcaps.release(); S->srch.release(); S->skeys.release(); S->sidx.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
