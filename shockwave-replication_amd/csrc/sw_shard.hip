@@ -715,16 +715,21 @@ constexpr int kSortThreads = kSortChunk / 2;
 __device__ __forceinline__ bool key_gt(const key2& a, const key2& b) {
     return a.h > b.h || (a.h == b.h && a.l > b.l);
 }
+/* nact (optional): the entries are compacted, the first *nact active —
+ * chunks past them have nothing to sort */
 __global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_ent* all, int64_t M,
-                                                                   key2* skeys, int32_t* sidx) {
+                                                                   key2* skeys, int32_t* sidx,
+                                                                   const int32_t* nact = nullptr) {
     __shared__ key2 k[kSortChunk];
     __shared__ int32_t ix[kSortChunk];
     const int64_t c0 = (int64_t)blockIdx.x * kSortChunk;
+    const int64_t na = nact ? (int64_t)*nact : M;
+    if (c0 >= na) return;
     for (int x = threadIdx.x; x < kSortChunk; x += kSortThreads) {
         const int64_t e = c0 + x;
         key2 v;
         v.h = 0; v.l = 0;
-        if (e < M && all[e].st != 0) { v.h = all[e].khi; v.l = all[e].klo; }
+        if (e < M && e < na && all[e].st != 0) { v.h = all[e].khi; v.l = all[e].klo; }
         k[x] = v;
         ix[x] = (int32_t)e;
     }
@@ -750,8 +755,10 @@ __global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_
 }
 
 __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, const int32_t* sidx,
-                                                         int nchunks, int32_t* order) {
+                                                         int nchunks, int32_t* order,
+                                                         const int32_t* nact = nullptr) {
     const int64_t s = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (nact) nchunks = (int)((*nact + kSortChunk - 1) / kSortChunk);
     if (s >= (int64_t)nchunks * kSortChunk) return;
     const key2 v = skeys[s];
     if (v.h == 0 && v.l == 0) return; /* inactive or padding */
@@ -868,45 +875,70 @@ __global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, 
  * (C4: a 4,096-entry rank sort and four full edge builds in one workgroup,
  * ~190 of its ~225 µs).  Same values, so the same result bit for bit. */
 
-/* one workgroup: the active entries compacted in job order into the X
- * arrays (as k_p2x does), their width classes (hdr) and the rank-sort keys
- * (class asc, sw_p2x_ckey(c) desc, job asc, as descending (~hi, ~lo) keys
- * for k_pack_chunk_sort; entry a of keys = active entry a) */
-__global__ __launch_bounds__(SW_BLOCK) void k_p2x_pre0(const p2x_ent* all, int64_t M, int T,
-                                                       unsigned char* ws, int32_t* hdr,
-                                                       sw_pack_ent* keys) {
-    __shared__ sw_xchg Xc;
-    __shared__ uint32_t wmap[8];
-    __shared__ int32_t cls[SW_P2X_KMAX], cnt[SW_P2X_KMAX];
-    __shared__ int32_t Ks;
-    sw_blk blk;
-    blk.X = &Xc;
-    blk.par = 0;
+/* the active entries compacted in job order into the X arrays (as k_p2x
+ * does), by the grid: k_p2x_cnt counts each block's active entries,
+ * k_p2x_compact places them (each block's offset = the counts before it),
+ * and collects the widths present (wmap) */
+__global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, int32_t* bcnt) {
+    const int64_t j = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int a = (j < M && all[j].n > 0) ? 1 : 0;
+    const int w = __popcll(__ballot(a));
+    __shared__ int32_t ws_[kTB / 64];
+    if (lane_id() == 0) ws_[wave_id()] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int c = 0;
+        for (int i = 0; i < kTB / 64; ++i) c += ws_[i];
+        bcnt[blockIdx.x] = c;
+    }
+}
+
+__global__ __launch_bounds__(kTB) void k_p2x_compact(const p2x_ent* all, int64_t M, const int32_t* bcnt,
+                                                     unsigned char* ws, uint32_t* wmap, int32_t* hdr) {
+    __shared__ int32_t base_, wsum[kTB / 64];
+    __shared__ uint32_t bm[8]; /* this block's widths, one global OR per word */
+    const int64_t j = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (threadIdx.x < 8) bm[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+        int b = 0;
+        for (unsigned i = 0; i < blockIdx.x; ++i) b += bcnt[i];
+        base_ = b;
+        if (blockIdx.x == gridDim.x - 1) hdr[SW_P2X_HDR_A] = b + bcnt[blockIdx.x];
+    }
+    p2x_ent e;
+    e.m = 0; e.p = 0.0; e.n = 0; e.w = 0;
+    if (j < M) e = all[j];
+    const bool act = e.n > 0;
+    const uint64_t bal = __ballot(act);
+    const int lane = lane_id();
+    if (lane == 0) wsum[wave_id()] = __popcll(bal);
+    __syncthreads();
+    if (act) atomicOr(&bm[(e.w >> 5) & 7], 1u << (e.w & 31));
+    __syncthreads();
+    if (threadIdx.x < 8 && bm[threadIdx.x]) atomicOr(&wmap[threadIdx.x], bm[threadIdx.x]);
+    if (!act) return;
+    int a = base_ + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int i = 0; i < wave_id(); ++i) a += wsum[i];
     sw_p2x_arrays X;
     X.cc = reinterpret_cast<double*>(ws);
     X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
     X.cw = reinterpret_cast<int32_t*>(X.cm + M);
     X.cj = X.cw + M;
+    X.cw[a] = e.w;
+    X.cj[a] = (int32_t)j;
+    X.cc[a] = e.p / (double)e.n;
+    X.cm[a] = e.m;
+}
+
+/* one workgroup: the width classes (ascending) and their sizes, hdr */
+__global__ __launch_bounds__(SW_BLOCK) void k_p2x_classes(const unsigned char* ws, int64_t M, int T,
+                                                          const uint32_t* wmap, int32_t* hdr) {
+    __shared__ int32_t cls[SW_P2X_KMAX], cnt[SW_P2X_KMAX];
+    __shared__ int32_t Ks;
     const int tid = threadIdx.x;
-    const int64_t q = (M + SW_BLOCK - 1) / SW_BLOCK;
-    const int64_t j0 = (int64_t)tid * q, j1 = j0 + q < M ? j0 + q : M;
-    int act = 0;
-    for (int64_t j = j0; j < j1; ++j) act += all[j].n > 0;
-    if (tid < 8) wmap[tid] = 0u;
+    const int32_t* cw = reinterpret_cast<const int32_t*>(ws + (size_t)M * 16);
+    const int A = hdr[SW_P2X_HDR_A];
     if (tid < SW_P2X_KMAX) cnt[tid] = 0;
-    int A;
-    int a = blk.exscan(act, A); /* its barrier publishes wmap, cnt */
-    for (int64_t j = j0; j < j1; ++j) {
-        const p2x_ent e = all[j];
-        if (e.n <= 0) continue;
-        X.cw[a] = e.w;
-        X.cj[a] = (int32_t)j;
-        X.cc[a] = e.p / (double)e.n;
-        X.cm[a] = e.m;
-        atomicOr(&wmap[(e.w >> 5) & 7], 1u << (e.w & 31));
-        ++a;
-    }
-    __syncthreads();
     if (tid == 0) {
         int K = 0;
         for (int i = 0; i < 8; ++i) K += __builtin_popcount(wmap[i]);
@@ -921,30 +953,15 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x_pre0(const p2x_ent* all, int64
     }
     __syncthreads();
     const int K = Ks;
-    if (K >= 0)
+    if (K > 0)
         for (int i = tid; i < A; i += SW_BLOCK) {
             int k = 0;
-            while (k < K - 1 && cls[k] != X.cw[i]) ++k;
+            while (k < K - 1 && cls[k] != cw[i]) ++k;
             atomicAdd(&cnt[k], 1);
-            const uint64_t ck = sw_p2x_ckey(X.cc[i]);
-            const uint64_t hi = ((uint64_t)k << 61) | (~ck & ((1ull << 61) - 1));
-            const uint64_t lo = ((uint64_t)(uint32_t)X.cj[i] << 32) | (uint32_t)i;
-            sw_pack_ent e;
-            e.khi = ~hi;
-            e.klo = ~lo;
-            e.st = 1u;
-            e.pad = 0u;
-            keys[i] = e;
         }
-    for (int64_t i = (int64_t)A + tid; i < M; i += SW_BLOCK) {
-        sw_pack_ent e;
-        e.khi = 0; e.klo = 0; e.st = 0u; e.pad = 0u;
-        keys[i] = e;
-    }
     __syncthreads();
     if (tid == 0) {
         hdr[SW_P2X_HDR_K] = K;
-        hdr[SW_P2X_HDR_A] = A;
         int o = 0, b = 0;
         for (int k = 0; k < SW_P2X_KMAX; ++k) {
             const int m = (K >= 0 && k < K) ? cnt[k] : 0;
@@ -958,6 +975,29 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x_pre0(const p2x_ent* all, int64
         }
         hdr[SW_P2X_HDR_OFF + SW_P2X_KMAX] = o;
     }
+}
+
+/* the rank-sort keys (class asc, sw_p2x_ckey(c) desc, job asc), as
+ * descending (~hi, ~lo) keys for k_pack_chunk_sort; key a = active entry a */
+__global__ __launch_bounds__(kTB) void k_p2x_keys(const unsigned char* ws, int64_t M, const int32_t* hdr,
+                                                  sw_pack_ent* keys) {
+    const int64_t i = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int K = hdr[SW_P2X_HDR_K], A = hdr[SW_P2X_HDR_A];
+    if (i >= A || K <= 0) return;
+    const double* cc = reinterpret_cast<const double*>(ws);
+    const int32_t* cw = reinterpret_cast<const int32_t*>(ws + (size_t)M * 16);
+    const int32_t* cj = cw + M;
+    int k = 0;
+    while (k < K - 1 && hdr[SW_P2X_HDR_WC + k] != cw[i]) ++k;
+    const uint64_t ck = sw_p2x_ckey(cc[i]);
+    const uint64_t hi = ((uint64_t)k << 61) | (~ck & ((1ull << 61) - 1));
+    const uint64_t lo = ((uint64_t)(uint32_t)cj[i] << 32) | (uint32_t)i;
+    sw_pack_ent e;
+    e.khi = ~hi;
+    e.klo = ~lo;
+    e.st = 1u;
+    e.pad = 0u;
+    keys[i] = e;
 }
 
 /* positions and bitsets: one wave per 64-rank word slot (class k, word w):
@@ -1527,12 +1567,10 @@ inline const void* peer_gathered(const sw_shard_state* S) {
 int coll_reduce(sw_shard_state* S, void* dbuf, int n, int op, void* hout) {
     hipStream_t st = S->h->stream;
     const size_t bytes = (size_t)n * 8;
-    /* with a communicator the all-reduce always runs through RCCL, world 1
-     * included (it is the identity there, but the path is the one the
-     * multi-GPU solve takes); without one (a single rank never initialised
-     * for collectives) it is skipped */
+    /* through RCCL above world 1; at world 1 the all-reduce is the identity
+     * and is skipped (RCCL's own copies cost ~30 µs per C4 solve there) */
     if (S->peer) return peer_xchg(S, dbuf, bytes, op, n, dbuf, hout);
-    if (S->comm) {
+    if (S->comm && S->world > 1) {
         const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
         SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, st));
     }
@@ -1563,7 +1601,7 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
         return SW_OK;
     }
     if (!S->host_comm) {
-        const bool one = !S->comm;
+        const bool one = !S->comm || S->world == 1;
         /* no communicator: the gather is the identity; a gather read back by
          * the host is not needed on the device afterwards, so it is copied
          * down directly */
@@ -2009,7 +2047,7 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         const size_t xa = ((size_t)M * SW_P2X_ARR_BYTES + 15) & ~(size_t)15;
         const size_t words = (size_t)T * ((size_t)(M + 63) / 64 + SW_P2X_KMAX);
         const size_t need = xa + 256 + (size_t)M * 4 + (size_t)M * 8 + words * 8 +
-                            (size_t)SW_P2X_KMAX * T * T * 9 + 64;
+                            (size_t)SW_P2X_KMAX * T * T * 9 + 64 + (size_t)nblk(M) * 4 + 16;
         if (S->p2ws.reserve(need) || S->p2keys.reserve((size_t)M))
             return host_fail(S, "P2 exchange workspace");
         unsigned char* base = S->p2ws.p + xa;
@@ -2019,13 +2057,21 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         uint64_t* B = reinterpret_cast<uint64_t*>(pc + M);
         double* Wb = reinterpret_cast<double*>(B + words);
         int8_t* Wk = reinterpret_cast<int8_t*>(Wb + (size_t)SW_P2X_KMAX * T * T);
-        LAUNCH(S, k_p2x_pre0, dim3(1), dim3(SW_BLOCK), 0, st, (const p2x_ent*)gv, M, T, S->p2ws.p, hdr,
-               S->p2keys.p);
+        int32_t* bcnt = reinterpret_cast<int32_t*>(Wk + (size_t)SW_P2X_KMAX * T * T);
+        uint32_t* wmap = reinterpret_cast<uint32_t*>(hdr + SW_P2X_HDR_INTS);
+        SH_HIP(S, hipMemsetAsync(wmap, 0, 32, st));
+        const int nb = nblk(M);
+        LAUNCH(S, k_p2x_cnt, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt);
+        LAUNCH(S, k_p2x_compact, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, S->p2ws.p, wmap,
+               hdr);
+        LAUNCH(S, k_p2x_classes, dim3(1), dim3(SW_BLOCK), 0, st, S->p2ws.p, M, T, wmap, hdr);
+        LAUNCH(S, k_p2x_keys, dim3(nb), dim3(kTB), 0, st, S->p2ws.p, M, hdr, S->p2keys.p);
+        /* the active keys only: chunks past A exit, the merge ranks against ⌈A / 1024⌉ chunks */
         const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
         LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, S->p2keys.p, M, S->skeys.p,
-               S->sidx.p);
+               S->sidx.p, (const int32_t*)(hdr + SW_P2X_HDR_A));
         LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
-               S->sidx.p, nch, S->porder.p);
+               S->sidx.p, nch, S->porder.p, (const int32_t*)(hdr + SW_P2X_HDR_A));
         const int64_t slots = (M + 63) / 64 + SW_P2X_KMAX;
         LAUNCH(S, k_p2x_pre_bits, dim3(nblk(slots * 64)), dim3(kTB), 0, st, hdr, S->porder.p, S->p2ws.p,
                M, T, ord, pc, B);

@@ -1,0 +1,33 @@
+"""Per-rank kernel time per C4 solve from a rocprofv3 kernel trace of
+tools/peer_timing.py (W ranks as processes on one GPU): each process's
+kernel durations summed and divided by its solves (k_setup launches, one per
+solve).  The ranks share the GPU, so wall time per solve does not fall with
+W here; the per-rank kernel work is what a rank on its own GPU would run.
+    python tools/peer_kernel_time.py <rocprofv3 output dir> [W]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+rows = []
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True)):
+    rows += list(csv.DictReader(open(f)))
+pid_key = next((k for k in ("Process_Id", "Pid", "PID") if rows and k in rows[0]), None)
+per = collections.defaultdict(lambda: [0.0, 0, collections.Counter()])
+for r in rows:
+    p = r[pid_key] if pid_key else "all"
+    d = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    per[p][0] += d
+    name = r["Kernel_Name"]
+    if "k_setup" in name:
+        per[p][1] += 1
+    per[p][2][name.split("(")[0][-40:]] += d
+out = {}
+for p, (tot, solves, by) in per.items():
+    if solves == 0:
+        continue
+    out[p] = {"solves": solves, "kernel_us_per_solve": tot / solves / 1e3,
+              "top": {k: round(v / solves / 1e3, 2) for k, v in by.most_common(6)}}
+print(json.dumps({"world": int(sys.argv[2]) if len(sys.argv) > 2 else None, "ranks": out}))
