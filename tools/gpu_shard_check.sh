@@ -16,8 +16,8 @@ rc=$?
 echo "exit $rc"; tail -3 $OUT/pytest_gpu.log; cat $OUT/bench_c4.json; cat $OUT/peer_w2.json $OUT/peer_w4.json
 [ $rc -eq 0 ] || exit $rc
 # per-rank kernel time at W = 2 / 4 (processes on one GPU)
-timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer2 -o run -- python3 tools/peer_timing.py 2 40 > $OUT/prof_peer2.log 2>&1 &&
-timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer4 -o run -- python3 tools/peer_timing.py 4 40 > $OUT/prof_peer4.log 2>&1 &&
+timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer2 -o run_%pid% -- python3 tools/peer_timing.py 2 40 > $OUT/prof_peer2.log 2>&1 &&
+timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer4 -o run_%pid% -- python3 tools/peer_timing.py 4 40 > $OUT/prof_peer4.log 2>&1 &&
 python3 tools/peer_kernel_time.py $OUT/prof_peer2 2 > $OUT/peer_kernel_w2.json &&
 python3 tools/peer_kernel_time.py $OUT/prof_peer4 4 > $OUT/peer_kernel_w4.json
 rc=$?

@@ -13,17 +13,18 @@ import sys
 
 rows = []
 for f in sorted(glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True)):
-    rows += list(csv.DictReader(open(f)))
-pid_key = next((k for k in ("Process_Id", "Pid", "PID") if rows and k in rows[0]), None)
+    for r in csv.DictReader(open(f)):
+        r["_file"] = os.path.basename(f)
+        rows.append(r)
 per = collections.defaultdict(lambda: [0.0, 0, collections.Counter()])
 for r in rows:
-    p = r[pid_key] if pid_key else "all"
+    p = f'{r["_file"]}:{r.get("Thread_Id", "")}'  # one launching thread per rank process
     d = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     per[p][0] += d
-    name = r["Kernel_Name"]
-    if "k_setup" in name:
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    if name.startswith("k_setup"):
         per[p][1] += 1
-    per[p][2][name.split("(")[0][-40:]] += d
+    per[p][2][name.split("(")[0].split("<")[0][:40]] += d
 out = {}
 for p, (tot, solves, by) in per.items():
     if solves == 0:
