@@ -51,7 +51,7 @@ static int split_min_count() {
 extern "C" size_t sw_plan_kernel_lds_bytes(int one);
 extern "C" hipError_t sw_launch_plan(const sw_batch_dev* B, int KT, int one, size_t lds,
                                      hipStream_t stream);
-extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream);
+extern "C" hipError_t sw_launch_split(sw_batch_dev* B, size_t p2x_lds, hipStream_t stream);
 extern "C" hipError_t sw_launch_p2x(const sw_batch_dev* B, int maxN, int maxT, hipStream_t stream);
 extern "C" size_t sw_p2x_kernel_lds_bytes(int maxN, int maxT);
 
@@ -492,9 +492,10 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
 #else
     const bool split = one && B.count > split_min_count();
 #endif
-    B.fuse_p2x = one && !split && B.count <= kFuseMaxCount;
+    B.fuse_p2x = one && (split || B.count <= kFuseMaxCount); /* split: always fused */
     if (B.fuse_p2x) lds = std::max(lds, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT));
-    hipError_t e = split ? sw_launch_split(&B, s) : sw_launch_plan(&B, B.KT, one, lds, s);
+    hipError_t e = split ? sw_launch_split(&B, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT), s)
+                         : sw_launch_plan(&B, B.KT, one, lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "plan kernel launch");
     if (timed) {
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], s));

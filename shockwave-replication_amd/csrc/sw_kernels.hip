@@ -1853,8 +1853,6 @@ struct RREnv {
 template <int KT, bool ONE>
 __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned char* smem,
                                                          int inst_) {
-    /* the slow-path launch after sw_pack_kernel: only the marked instances */
-    if (B.only_slow && !(B.out[inst_].status & SW_STATUS_SLOW_MARK)) return;
     const sw_inst_dev* I = &B.inst[inst_];
 #ifdef SW_STAMPS
     /* placement diagnostics: 100 MHz wall clock at entry / exit, HW_ID, XCC_ID */
@@ -2312,6 +2310,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
 template <int KT, bool ONE>
 __global__ __launch_bounds__(SW_BLOCK) void sw_plan_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
+    /* the slow-path launch after sw_pack_kernel: only the marked instances
+     * (the rest were solved, and exchanged, there) */
+    if (B.only_slow && !(B.out[blockIdx.x].status & SW_STATUS_SLOW_MARK)) return;
     solve_instance<KT, ONE>(B, sw_smem, blockIdx.x);
     if constexpr (ONE) {
         /* one launch for the whole batch: the instance's P2 exchange step
@@ -2332,10 +2333,20 @@ __global__ __launch_bounds__(SW_BLOCK, 4) void sw_level_kernel(sw_batch_dev B) {
     level_instance<KT>(B, sw_smem, blockIdx.x);
 }
 
-/* ≤ 64 VGPRs, ~35 KB of LDS: four 512-thread workgroups per CU */
+/* ≤ 64 VGPRs, ~37 KB of LDS: four 512-thread workgroups per CU.  The
+ * instance's P2 exchange step follows its emit in the same workgroup (the
+ * pack state is dead by then, its LDS is the step's): the pack's round loop
+ * keeps one wave of eight busy, the exchange all eight, so on a CU whose
+ * workgroups are in different phases the exchanges fill the issue slots the
+ * round loops leave idle — where two kernels ran the loops of every instance
+ * first and all the exchanges after them. */
 __global__ __launch_bounds__(SW_BLOCK, 8) void sw_pack_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
     pack_instance(B, sw_smem, blockIdx.x);
+    if (B.fuse_p2x) {
+        __syncthreads(); /* the emit's masks and status are visible */
+        if (!(B.out[blockIdx.x].status & SW_STATUS_SLOW_MARK)) sw_p2x_instance(B, B.p2ws, sw_smem, blockIdx.x);
+    }
 }
 
 /* LDS bytes the kernel needs (solve_instance checks its carve-up against it). */
@@ -2344,14 +2355,18 @@ extern "C" size_t sw_plan_kernel_lds_bytes(int one) { return sw_plan_lds_bytes(o
 /* The split path for on-chip batches (every instance N ≤ SW_LDS_JOBS and
  * T ≤ 32): level search, then pack + emit, then the full kernel for the
  * instances the pack kernel marked (B->only_slow set by the caller). */
-extern "C" hipError_t sw_launch_split(sw_batch_dev* B, hipStream_t stream) {
+/* Every instance's exchange step runs inside these launches: the pack
+ * kernel's instances at its end, the marked ones at the end of the full
+ * kernel (p2x_lds: the step's LDS for the batch's largest instance). */
+extern "C" hipError_t sw_launch_split(sw_batch_dev* B, size_t p2x_lds, hipStream_t stream) {
     dim3 grid(B->count), block(SW_BLOCK);
     B->only_slow = 0;
+    B->fuse_p2x = 1;
     hipLaunchKernelGGL((sw_level_kernel<32>), grid, block, sw_level_lds_bytes(), stream, *B);
-    hipLaunchKernelGGL(sw_pack_kernel, grid, block, sw_pack_lds_bytes(), stream, *B);
+    hipLaunchKernelGGL(sw_pack_kernel, grid, block, std::max(sw_pack_lds_bytes(), p2x_lds), stream, *B);
     B->only_slow = 1;
-    B->fuse_p2x = 0; /* sw_p2x_kernel follows for every instance */
-    hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, sw_plan_lds_bytes(true), stream, *B);
+    hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, std::max(sw_plan_lds_bytes(true), p2x_lds),
+                       stream, *B);
     B->only_slow = 0;
     return hipGetLastError();
 }

@@ -1,12 +1,13 @@
 """The P2 placement cascade on the GPU: batched kernel (on-chip and
-HBM-workspace paths) and the sharded engine against the CPU twin, bit for bit,
-on the captured simulator instances (tests/golden/p2_cases.json)."""
+HBM-workspace paths) against the CPU twin, and the sharded engine against the
+CPU shard engine, bit for bit, on the captured simulator instances
+(tests/golden/p2_cases.json)."""
 import pytest
 
 from helpers import assert_same_result, check_plan_valid
 from p2cases import arrays, load_cases
 from test_gpu_shard import gpu_shard_threads
-from test_shard import assert_same_as_single
+from test_shard import assert_same_as_single, assert_share_contract, run_threads, shard_lib  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 CASES = load_cases()
@@ -36,6 +37,13 @@ def test_gpu_p2_batched_mixed(gpu_solver, twin):
 
 
 @pytest.mark.parametrize("i,tile,world", [(3, 1, 2), (6, 1, 2), (4, 8, 2)])
-def test_gpu_shard_p2_cascade(twin, i, tile, world):
+def test_gpu_shard_p2_cascade(shard_lib, twin, i, tile, world):  # noqa: F811
+    """The sharded contract: the GPU shard engine equals the
+    CPU shard engine at the same world size bit for bit; against the single
+    instance, P1 bit for bit and the share placement's P2 within its ratio."""
     a = arrays(CASES[i], tile)
-    assert_same_as_single(gpu_shard_threads(a, world), twin.solve(a), f"case {i} x{tile} W={world}")
+    rg = gpu_shard_threads(a, world)
+    check_plan_valid(a, rg)
+    what = f"case {i} x{tile} W={world}"
+    assert_same_as_single(rg, run_threads(shard_lib, a, world), what)
+    assert_share_contract(rg, twin.solve(a), what)
