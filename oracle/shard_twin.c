@@ -86,7 +86,7 @@ static int lanes_gather(eng_t* E, const double* v, double* out) {
     return rc;
 }
 
-static int e_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
+static int e_setup(void* ctx, double* A, double* lb, double* top) {
     eng_t* E = (eng_t*)ctx;
     double mx[3] = {0.0, 0.0, 0.0};
     for (int32_t i = 0; i < E->NL; ++i) mx[0] = sw_max(mx[0], E->jc[i].a);
@@ -109,20 +109,25 @@ static int e_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all
     *A = E->A;
     *lb = mx[1];
     *top = mx[2];
-    /* widths of every job, gathered in padded per-rank blocks */
+    /* widths of every job, gathered in padded per-rank blocks (the gathered
+     * placements read them; the controller asks for them through e_widths) */
     int32_t* blk = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1), sizeof(int32_t));
     int32_t* all = (int32_t*)calloc((size_t)(E->P > 0 ? E->P : 1) * E->world, sizeof(int32_t));
     if (!blk || !all) { free(blk); free(all); return -1; }
     for (int32_t i = 0; i < E->NL; ++i) blk[i] = E->jc[i].w;
     int rc = E->comm->allgather(E->comm->ctx, blk, all, E->P * (int64_t)sizeof(int32_t));
     /* rank r's block starts at r·P, which is also its first global job */
-    for (int64_t j = 0; j < E->N; ++j) {
-        w_all[j] = all[j];
-        E->w_all[j] = all[j];
-    }
+    for (int64_t j = 0; j < E->N; ++j) E->w_all[j] = all[j];
     free(blk); free(all);
     return rc;
 }
+
+static int e_widths(void* ctx, int32_t* w_all) {
+    eng_t* E = (eng_t*)ctx;
+    for (int64_t j = 0; j < E->N; ++j) w_all[j] = E->w_all[j];
+    return 0;
+}
+
 
 static int e_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
     eng_t* E = (eng_t*)ctx;
@@ -670,6 +675,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     sw_shard_ops ops;
     ops.ctx = &E;
     ops.setup = e_setup;
+    ops.widths = e_widths;
     ops.force = e_force;
     ops.count_gt = e_count_gt;
     ops.feasible = e_feasible;

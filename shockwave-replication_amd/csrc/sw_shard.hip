@@ -77,10 +77,11 @@ constexpr int kTB = 256;  /* threads per block of the per-job kernels */
 constexpr int kRed = 128; /* entries of the step-result buffer        */
 constexpr int kRing = 64; /* step-result slices cleared together      */
 constexpr int kProbeBlocks = 256; /* grid of the K-ary probe kernels       */
-/* capacity rows a pack stages (pinned host row → device row, asynchronous):
- * a row is rewritten kCapsRows packs later, and at most 8 class packs plus
- * one share pack are enqueued between two host-synchronised steps */
-constexpr uint32_t kCapsRows = 16;
+/* a pack's per-round capacities, passed by value (no staging copy) */
+struct CapsArg {
+    int32_t v[SW_TMAX];
+    int32_t has; /* 0: capacity G in every round */
+};
 
 struct sw_pack_ent {
     uint64_t khi, klo; /* order key (desc); klo low 32 bits = ~job */
@@ -687,9 +688,16 @@ __global__ __launch_bounds__(kTB) void k_load(ShardDev S, const int32_t* src) {
     red_add(S.red, v);
 }
 
-/* per-solve state: every count array, every bitmask, l and taken = 0 */
+__global__ __launch_bounds__(kTB) void k_copy_words(uint32_t* dst, const uint32_t* src, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+/* per-solve state: every count array, every bitmask, l and taken = 0, and the
+ * step-result ring (S.red at its base) */
 __global__ __launch_bounds__(kTB) void k_zero_state(ShardDev S) {
     const int i = blockIdx.x * kTB + threadIdx.x;
+    if (i < kRing * kRed) S.red[i] = 0;
     if (i >= S.NL) return;
 #pragma unroll
     for (int a = 0; a < SW_A_COUNT; ++a) S.arr[a][i] = 0;
@@ -778,12 +786,12 @@ __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, cons
 }
 
 /* the round loop over the global order; writes this rank's rows */
-/* capsd: per-round capacities of the class-wise repack (nullptr = G); then
- * only the entries' rows are written, every other job is left untouched */
+/* has_caps: per-round capacities in capsL (the share placement's shares, a
+ * class-wise repack's class capacities), else G */
 template <int E, class BLK>
 __device__ __forceinline__ void pack_rounds_body(const ShardDev& S, const sw_pack_ent* all, int A,
                                                  const int32_t* order, uint64_t* ydst, int32_t* pdst,
-                                                 const int32_t* capsd, BLK& blk, sw_pack_lds* PL,
+                                                 bool has_caps, BLK& blk, sw_pack_lds* PL,
                                                  const int32_t* capsL) {
     const int tid = threadIdx.x;
     uint32_t st[E];
@@ -799,9 +807,9 @@ __device__ __forceinline__ void pack_rounds_body(const ShardDev& S, const sw_pac
         ent[i] = E * tid + i < A ? ent[i] : -1;
     }
 #ifdef SW_STAMPS
-    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr, g_sw_pack_stamps);
+    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, has_caps ? capsL : nullptr, g_sw_pack_stamps);
 #else
-    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, capsd ? capsL : nullptr);
+    sw_pack_rounds<E>(blk, PL, A, S.T, S.G, st, mk, has_caps ? capsL : nullptr);
 #endif
 #pragma unroll
     for (int i = 0; i < E; ++i) {
@@ -829,7 +837,7 @@ template <int E, int NT>
 __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
                                                     int64_t M, const int32_t* order,
                                                     uint64_t* ydst, int32_t* pdst,
-                                                    const int32_t* capsd, int alo, int zero) {
+                                                    CapsArg caps, int alo, int zero) {
     __shared__ sw_xchg_t<NT / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
@@ -837,14 +845,90 @@ __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_en
     blk.X = &X;
     blk.par = 0;
     const int tid = threadIdx.x;
-    if (capsd && tid < S.T) capsL[tid] = capsd[tid];
+    if (caps.has && tid < S.T) capsL[tid] = caps.v[tid];
     int act = 0;
     for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
     if (A <= alo || A > E * NT) return; /* the other variant places these */
     if (zero) /* a whole placement (not one width class): every row of this rank */
         for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
-    pack_rounds_body<E>(S, all, A, order, ydst, pdst, capsd, blk, &PL, capsL);
+    pack_rounds_body<E>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+}
+
+/* The same round loop on ONE wave (sw_pack_rounds_wave, sw_pack.h): E1
+ * positions per lane, position p = E1·lane + i, no barriers — for placements
+ * with at most kWaveA active entries, where the block loop's two barriers per
+ * scan cost more than the wave's longer per-lane walks (the share placement
+ * of a rank's own jobs at W ≥ 2, the class repacks).  A runtime E1 over four
+ * instantiations: one wave per CU, so the widest one's registers cost
+ * nothing. */
+constexpr int kWaveE = 64;
+template <int E1>
+__device__ __forceinline__ void pack_rounds_wave_body(const ShardDev& S, const sw_pack_ent* all, int A,
+                                                      const int32_t* order, uint64_t* ydst, int32_t* pdst,
+                                                      const int32_t* capsL, sw_pack_lds* PL, uint64_t* xmk) {
+    const int lane = lane_id();
+    uint32_t st[E1];
+    int32_t ent[E1];
+#pragma unroll
+    for (int i = 0; i < E1; ++i) {
+        const int p = E1 * lane + i;
+        ent[i] = p < A ? order[p] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < E1; ++i) st[i] = ent[i] >= 0 ? all[ent[i]].st : 0u;
+    sw_pack_rounds_wave<E1>(PL, S.T, S.G, st, xmk, capsL);
+#pragma unroll
+    for (int i = 0; i < E1; ++i) {
+        if (ent[i] < 0) continue;
+        const sw_pack_ent& e = all[ent[i]];
+        const int64_t j = (int64_t)(0xFFFFFFFFu - (uint32_t)(e.klo & 0xFFFFFFFFu));
+        if (j >= S.off && j < S.off + S.NL) {
+            ydst[j - S.off] = xmk[E1 * lane + i];
+            pdst[j - S.off] = (int32_t)(e.st & 0xFFu) - (int32_t)pk_r(st[i]);
+        }
+    }
+}
+
+/* amax: the largest active count this kernel places (≤ 64·kWaveE); the block
+ * variants (k_pack_rounds, alo = amax) place larger ones */
+__global__ __launch_bounds__(64) void k_pack_rounds_wave(ShardDev S, const sw_pack_ent* all, int64_t M,
+                                                         const int32_t* order, uint64_t* ydst, int32_t* pdst,
+                                                         CapsArg caps, int amax, int zero) {
+    __shared__ sw_pack_lds PL;
+    __shared__ int32_t capsL[64];
+    __shared__ uint64_t xmk[64 * kWaveE];
+    const int lane = lane_id();
+    if (caps.has && lane < S.T) capsL[lane] = caps.v[lane];
+    int act = 0;
+    for (int64_t e = lane; e < M; e += 64) act += all[e].st != 0;
+    const int A = wave_sum_i32(act);
+    if (A > amax) return; /* the block variant places these */
+    if (zero) /* a whole placement (not one width class): every row of this rank */
+        for (int i = lane; i < S.NL; i += 64) { ydst[i] = 0; pdst[i] = 0; }
+    __threadfence_block(); /* the zero rows land before the placed rows below */
+    wave_sync();           /* capsL */
+    const int32_t* cl = caps.has ? capsL : nullptr;
+    if (A <= 64 * 8) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
+    else if (A <= 64 * 16) pack_rounds_wave_body<16>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
+    else if (A <= 64 * 32) pack_rounds_wave_body<32>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
+    else pack_rounds_wave_body<64>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
+}
+
+/* Active entries up to which the one-wave loop places (SW_SHARD_WAVE_A
+ * overrides; 0 = never).  Measured on C4's share placement (MI355X,
+ * profiles/r7c4w1_*): 1,900 active entries per rank (W = 2) take 214 µs in
+ * the wave loop (E1 = 32) against 149 µs in the 512-thread loop, 3,748 (W = 1)
+ * 0.98 ms per solve against 0.75 — its LDS histogram atomics serialise over
+ * the lanes of the wave — so it is kept to E1 = 8, where the block loop's
+ * two barriers per scan are most of a round's cost. */
+int wave_pack_max() {
+    static const int v = [] {
+        const char* e = getenv("SW_SHARD_WAVE_A");
+        const int x = e ? atoi(e) : 512;
+        return x < 0 ? 0 : (x > 64 * kWaveE ? 64 * kWaveE : x);
+    }();
+    return v;
 }
 
 /* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
@@ -879,8 +963,10 @@ __global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, 
  * does), by the grid: k_p2x_cnt counts each block's active entries,
  * k_p2x_compact places them (each block's offset = the counts before it),
  * and collects the widths present (wmap) */
-__global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, int32_t* bcnt) {
+__global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, int32_t* bcnt,
+                                                 uint32_t* wmap) {
     const int64_t j = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 8) wmap[threadIdx.x] = 0u; /* k_p2x_compact ORs into it */
     const int a = (j < M && all[j].n > 0) ? 1 : 0;
     const int w = __popcll(__ballot(a));
     __shared__ int32_t ws_[kTB / 64];
@@ -1423,7 +1509,6 @@ struct sw_shard_state {
     DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry), prepared set-up */
     DevBuf<sw_pack_ent> p2keys; /* the exchange's rank-sort keys (k_p2x_pre0) */
     DevBuf<unsigned char> rrin, rrrow, rrws; /* re-optimisation: gathered entries, workspace */
-    DevBuf<int32_t> caps; /* class-wise P2 capacities */
     DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
     DevBuf<int32_t> sidx; /* their entries */
@@ -1435,8 +1520,6 @@ struct sw_shard_state {
     bool zero_pending = false;
     /* pinned staging */
     HostBuf<uint8_t> hx;
-    HostBuf<int32_t> hcaps;
-    uint32_t caps_row = 0; /* next staging row of hcaps / caps (pack_any) */
     int32_t scaps[SW_TMAX]; /* this rank's share of every round (op_pack_share) */
     bool share = false;
     std::vector<int32_t> w_all;
@@ -1651,7 +1734,7 @@ int zero_red(sw_shard_state* S, int n) {
 
 /* ---- sw_shard_ops ---------------------------------------------------------- */
 
-int op_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
+int op_setup(void* ctx, double* A, double* lb, double* top) {
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
     SH_TRY(zero_red(S, 4));
@@ -1669,7 +1752,13 @@ int op_setup(void* ctx, double* A, double* lb, double* top, int32_t* w_all) {
     *A = sw_from_bits(mx[0]);
     *lb = sw_from_bits(mx[1]);
     *top = sw_from_bits(mx[3]);
-    /* every job's width, gathered once (the width tail needs w of the winner) */
+    return SW_OK;
+}
+
+/* every job's width (the controller's width tail and fill, on first use) */
+int op_widths(void* ctx, int32_t* w_all) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
     /* in place: this rank's block of the receive buffer is the send buffer
      * (no self-copy in the all-gather, none at all at world 1) */
     int32_t* wrecv = (int32_t*)S->xrecv.p;
@@ -1868,19 +1957,24 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     return SW_OK;
 }
 
+/* the controller's array copies: a kernel launch (a D2D hipMemcpyAsync
+ * costs the host several times a launch's enqueue, on the solve's critical
+ * path between two host-synchronised steps) */
 int op_copy(void* ctx, int32_t dst, int32_t src) {
     auto* S = (sw_shard_state*)ctx;
     if (S->NL)
-        SH_HIP(S, hipMemcpyAsync(S->arr[dst].p, S->arr[src].p, (size_t)S->NL * 4,
-                                 hipMemcpyDeviceToDevice, S->h->stream));
+        LAUNCH(S, k_copy_words, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream,
+               reinterpret_cast<uint32_t*>(S->arr[dst].p), reinterpret_cast<const uint32_t*>(S->arr[src].p),
+               (int64_t)S->NL);
     return SW_OK;
 }
 
 int op_copy_y(void* ctx, int32_t dst, int32_t src) {
     auto* S = (sw_shard_state*)ctx;
     if (S->NL)
-        SH_HIP(S, hipMemcpyAsync(S->y[dst].p, S->y[src].p, (size_t)S->NL * 8,
-                                 hipMemcpyDeviceToDevice, S->h->stream));
+        LAUNCH(S, k_copy_words, dim3(nblk(2 * (int64_t)S->NL)), dim3(kTB), 0, S->h->stream,
+               reinterpret_cast<uint32_t*>(S->y[dst].p), reinterpret_cast<const uint32_t*>(S->y[src].p),
+               2 * (int64_t)S->NL);
     return SW_OK;
 }
 
@@ -1890,14 +1984,11 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
              int32_t wc, const int32_t* caps, bool local = false) {
     hipStream_t st = S->h->stream;
     const int64_t M = local ? S->P : S->P * S->world;
-    const int32_t* capsd = nullptr;
+    CapsArg capsd;
+    memset(&capsd, 0, sizeof(capsd));
     if (caps) {
-        /* a staging row of its own (kCapsRows), so no synchronisation */
-        int32_t* hc = S->hcaps.p + (size_t)(S->caps_row++ % kCapsRows) * 64;
-        memcpy(hc, caps, (size_t)S->T * 4);
-        int32_t* dc = S->caps.p + (size_t)((S->caps_row - 1) % kCapsRows) * 64;
-        SH_HIP(S, hipMemcpyAsync(dc, hc, (size_t)S->T * 4, hipMemcpyHostToDevice, st));
-        capsd = dc;
+        memcpy(capsd.v, caps, (size_t)S->T * 4);
+        capsd.has = 1;
     }
     LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
            (int)wc, S->pall.p + (size_t)S->rank * S->P);
@@ -1919,18 +2010,28 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
 #define SW_LAUNCH_PACK(E, NT, ALO)                                                              \
     LAUNCH(S, (k_pack_rounds<E, NT>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, \
            pd, capsd, (int)(ALO), (int)(mode != 5))
-    if (M <= 2 * SW_BLOCK) {
-        SW_LAUNCH_PACK(2, SW_BLOCK, -1);
+    /* the one-wave loop for up to wa active entries, launched when the
+     * entries are few enough that most placements fit it (all of them when
+     * M ≤ wa: then no block variant is launched) */
+    const int wa = wave_pack_max();
+    const bool wave = wa > 0 && M <= 4 * (int64_t)wa;
+    if (wave)
+        LAUNCH(S, k_pack_rounds_wave, dim3(1), dim3(64), 0, st, dv, all, M, S->porder.p, yd, pd, capsd, wa,
+               (int)(mode != 5));
+    const int lo = wave ? wa : -1;
+    if (wave && M <= wa) {
+    } else if (M <= 2 * SW_BLOCK) {
+        SW_LAUNCH_PACK(2, SW_BLOCK, lo);
     } else if (M <= 8 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
     } else if (M <= 20 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
         SW_LAUNCH_PACK(20, SW_BLOCK, 8 * SW_BLOCK);
     } else if (M <= 32 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
         SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
     } else if (M <= 64 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, -1);
+        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
         SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
     } else {
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
@@ -2059,9 +2160,8 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         int8_t* Wk = reinterpret_cast<int8_t*>(Wb + (size_t)SW_P2X_KMAX * T * T);
         int32_t* bcnt = reinterpret_cast<int32_t*>(Wk + (size_t)SW_P2X_KMAX * T * T);
         uint32_t* wmap = reinterpret_cast<uint32_t*>(hdr + SW_P2X_HDR_INTS);
-        SH_HIP(S, hipMemsetAsync(wmap, 0, 32, st));
         const int nb = nblk(M);
-        LAUNCH(S, k_p2x_cnt, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt);
+        LAUNCH(S, k_p2x_cnt, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, wmap);
         LAUNCH(S, k_p2x_compact, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, S->p2ws.p, wmap,
                hdr);
         LAUNCH(S, k_p2x_classes, dim3(1), dim3(SW_BLOCK), 0, st, S->p2ws.p, M, T, wmap, hdr);
@@ -2148,7 +2248,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->xa.reserve(2 * NL) || S->plan.reserve(NL * T) ||
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
-               S->porder.reserve(M) || S->caps.reserve(64 * kCapsRows) || S->hcaps.reserve(64 * kCapsRows) ||
+               S->porder.reserve(M) || 
                S->srch.reserve(8) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
@@ -2192,9 +2292,11 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     if (dev && res->plan) v.plan = res->plan; /* the final step writes the caller's HBM */
     if (dev && res->planned_rounds) v.planned = res->planned_rounds;
     S->ring_pos = kRing; /* the first step clears the ring */
-    if (S->zero_pending) {
-        LAUNCH(S, k_zero_state, dim3(nblk(S->NL)), dim3(kTB), 0, st, v);
+    if (S->zero_pending) { /* the state, and the ring with it */
+        LAUNCH(S, k_zero_state, dim3(nblk(std::max<int64_t>(S->NL, (int64_t)kRing * kRed))), dim3(kTB), 0, st,
+               v);
         S->zero_pending = false;
+        S->ring_pos = 0;
     }
     return SW_OK;
 }
@@ -2232,7 +2334,7 @@ void sw_shard_release(sw_handle* h) {
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
     S->p2keys.release();
-    S->caps.release(); S->hcaps.release(); S->srch.release(); S->skeys.release(); S->sidx.release();
+    S->srch.release(); S->skeys.release(); S->sidx.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
@@ -2500,6 +2602,7 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     sw_shard_ops ops;
     ops.ctx = S;
     ops.setup = op_setup;
+    ops.widths = op_widths;
     ops.force = op_force;
     ops.count_gt = op_count_gt;
     ops.feasible = op_feasible;

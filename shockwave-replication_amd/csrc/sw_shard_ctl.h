@@ -75,8 +75,11 @@ enum {
 typedef struct sw_shard_ops {
     void* ctx;
     /* constants, key rows; A = max_j a_j, lb = max_j g_j(T_j), top = max_j
-     * g_j(0); w_all[N] = every job's width (gathered) */
-    int (*setup)(void* ctx, double* A, double* lb, double* top, int32_t* w_all);
+     * g_j(0) */
+    int (*setup)(void* ctx, double* A, double* lb, double* top);
+    /* w_all[N] = every job's width (gathered) — only the width tail and the
+     * fill need it, so it is gathered when one of them first runs */
+    int (*widths)(void* ctx, int32_t* w_all);
     /* l_j := #{n < T_j : g_j(n) > M} (0 if is_inf); out = (Σ w·l, Σ w·(T_j − l)) */
     int (*force)(void* ctx, double M, int32_t is_inf, int64_t out[2]);
     /* out[i] = Σ w·#{n ∈ [l_j, T_j) : key_j(n) > rho[i]} */
@@ -228,6 +231,7 @@ typedef struct {
     int64_t C;
     double k, A, lb, top;
     int32_t* w_all;
+    int w_ok;      /* w_all gathered */
     int64_t steps; /* collective steps taken (reported as iters) */
     double lanesA[SW_DET_LANES], lanesB[SW_DET_LANES];
 } sw_shard_ctl;
@@ -288,6 +292,17 @@ static inline int swc_search(sw_shard_ctl* c, int kind, uint64_t lo, uint64_t hi
     return 0;
 }
 
+/* job j's width, the widths gathered on first use (one collective step) */
+static inline int swc_width(sw_shard_ctl* c, int64_t j, int32_t* w) {
+    if (!c->w_ok) {
+        SWC_TRY(c->ops->widths(c->ops->ctx, c->w_all));
+        c->steps++;
+        c->w_ok = 1;
+    }
+    *w = c->w_all[j];
+    return 0;
+}
+
 /* twin: select_level ([plo, phi] brackets ρ*(M), see there) */
 static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eval* ev,
                              uint32_t plo, uint32_t phi) {
@@ -328,7 +343,9 @@ static inline int swc_select(sw_shard_ctl* c, double M, int is_inf, sw_shard_eva
             if (best == 0) break;
             const int64_t jb = (int64_t)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu));
             SWC_TRY(o->tail_apply(o->ctx, jb));
-            rem2 -= c->w_all[jb];
+            int32_t wb;
+            SWC_TRY(swc_width(c, jb, &wb));
+            rem2 -= wb;
         }
     }
     double gm;
@@ -529,6 +546,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
     c->C = (int64_t)G * T;
     c->k = k;
     c->steps = 0;
+    c->w_ok = 0;
     c->w_all = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
     int rc = 0;
     if (!c->w_all) { free(c); return -1; }
@@ -538,7 +556,7 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
         if (rc < 0) goto done;       \
     } while (0)
     {
-        SWC_RUN(o->setup(o->ctx, &c->A, &c->lb, &c->top, c->w_all));
+        SWC_RUN(o->setup(o->ctx, &c->A, &c->lb, &c->top));
         c->steps++;
         int32_t status = 0;
         double bound = 0.0, Jbest = 0.0, gm;
@@ -656,7 +674,9 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
                 const int64_t jb = sw_fill_job(best);
                 const int32_t tb = sw_fill_round(best);
                 SWC_RUN(o->fill_apply(o->ctx, jb, tb));
-                load[tb] += c->w_all[jb];
+                int32_t wb;
+                SWC_RUN(swc_width(c, jb, &wb));
+                load[tb] += wb;
                 ++added;
             }
             if (added > 0) {

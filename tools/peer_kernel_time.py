@@ -3,6 +3,8 @@ tools/peer_timing.py (W ranks as processes on one GPU): each process's
 kernel durations summed and divided by its solves (k_setup launches, one per
 solve).  The ranks share the GPU, so wall time per solve does not fall with
 W here; the per-rank kernel work is what a rank on its own GPU would run.
+k_xchg (the peer exchange) spends most of its time waiting for the other
+ranks' flags, so the work is also reported without it ("excl_xchg").
     python tools/peer_kernel_time.py <rocprofv3 output dir> [W]"""
 import collections
 import csv
@@ -29,6 +31,9 @@ out = {}
 for p, (tot, solves, by) in per.items():
     if solves == 0:
         continue
-    out[p] = {"solves": solves, "kernel_us_per_solve": tot / solves / 1e3,
-              "top": {k: round(v / solves / 1e3, 2) for k, v in by.most_common(6)}}
-print(json.dumps({"world": int(sys.argv[2]) if len(sys.argv) > 2 else None, "ranks": out}))
+    out[p] = {"solves": solves, "kernel_us_per_solve": round(tot / solves / 1e3, 2),
+              "kernel_us_per_solve_excl_xchg": round((tot - by.get("k_xchg", 0.0)) / solves / 1e3, 2),
+              "top": {k: round(v / solves / 1e3, 2) for k, v in by.most_common(8)}}
+ex = [v["kernel_us_per_solve_excl_xchg"] for v in out.values()]
+print(json.dumps({"world": int(sys.argv[2]) if len(sys.argv) > 2 else None,
+                  "mean_excl_xchg_us": round(sum(ex) / len(ex), 2) if ex else None, "ranks": out}))
