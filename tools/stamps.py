@@ -32,6 +32,10 @@ def main():
         "g64_900x20_k10": [ss.synth_problem(i, 900, 64, 20, 120.0, 10.0, 5.0) for i in range(16)],
         "g128_900x20_k1e-3": [ss.synth_problem(i, 900, 128, 20, 120.0, 1e-3, 15.0) for i in range(16)],
     }
+    if "--c5" in sys.argv:  # the C5 sweep's 512 instances (bench.c5_leg's problems)
+        sys.path.insert(0, ROOT)
+        import bench
+        cases = {"c5_sweep": ss.sweep_problems(bench.C5_INSTANCES, 900, seed0=bench.C5_SEED0, T_override=30)}
     if "--c4" in sys.argv:  # the C4 instance alone (workspace path; its exchange at 10k jobs)
         cases = {"c4_10000x30": [ss.synth_problem(77, 10000, 2848, 30, 120.0, 1e5, 5.0)]}
     names = ["setup", "p1_level_search", "p1_pack", "p1_misc", "p2_pack", "emit"]
@@ -70,6 +74,14 @@ def main():
         print("   P2 exchange kernel (sw_p2x_kernel):", " ".join(
             f"{n} {px[:, i].mean():.0f}" for i, n in enumerate(pn)),
             f"| total {px[:, :7].sum(axis=1).mean():.0f}")
+        if "--c5" in sys.argv:  # the slowest instances: solve + exchange cycles
+            tot_i = st.sum(axis=1) + px[:, :7].sum(axis=1)
+            print("   slowest instances (G, k, passes, status | solve phases | exchange phases, bf_iters, builds):")
+            for i in np.argsort(-tot_i)[:12]:
+                a = batch[i]
+                print(f"     #{i:3d} G {a.G:3d} k {a.k:g} it {res[i]['iters']:4d} st {res[i]['status']:4d} total "
+                      f"{tot_i[i]:9.0f} |", " ".join(f"{v:8.0f}" for v in st[i]), "|",
+                      " ".join(f"{v:8.0f}" for v in px[i, :9]))
         if "-v" in sys.argv:  # per-instance rows: status, passes, phase cycles
             for r, row, prow in list(zip(res, st, pk))[:24]:
                 print("     st", r["status"], "it", r["iters"], " ".join(f"{v:9.0f}" for v in row), "|",
