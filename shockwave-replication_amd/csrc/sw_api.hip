@@ -29,8 +29,14 @@
 #include "sw_validate.h"
 
 /* on-chip batches up to this many instances (one per CU) fuse the exchange
- * step into the full kernel */
-constexpr int kFuseMaxCount = 256;
+ * step into the full kernel (SW_FUSE_MAX overrides) */
+static int fuse_max_count() {
+    static const int v = [] {
+        const char* e = getenv("SW_FUSE_MAX");
+        return e ? atoi(e) : 256;
+    }();
+    return v;
+}
 
 /* On-chip batches above this many instances take the split kernels
  * (SW_SPLIT_MIN overrides).  The split buys several instances per CU in the
@@ -42,7 +48,7 @@ constexpr int kFuseMaxCount = 256;
 static int split_min_count() {
     static const int v = [] {
         const char* e = getenv("SW_SPLIT_MIN");
-        return e ? atoi(e) : 1024;
+        return e ? atoi(e) : 256;
     }();
     return v;
 }
@@ -492,7 +498,7 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
 #else
     const bool split = one && B.count > split_min_count();
 #endif
-    B.fuse_p2x = one && (split || B.count <= kFuseMaxCount); /* split: always fused */
+    B.fuse_p2x = one && (split || B.count <= fuse_max_count()); /* split: always fused */
     if (B.fuse_p2x) lds = std::max(lds, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT));
     hipError_t e = split ? sw_launch_split(&B, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT), s)
                          : sw_launch_plan(&B, B.KT, one, lds, s);
