@@ -359,8 +359,10 @@ def main():
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     # the solve's kernels, timed with HIP events on the handle's stream: the
-    # plan stage (sw_level_kernel + sw_pack_kernel + sw_plan_kernel for the
-    # instances the pack kernel leaves) and the P2 exchange (sw_p2x_kernel)
+    # plan stage (sw_level_kernel + sw_pack_kernel, which runs each instance's
+    # P2 exchange step after its pack, + sw_plan_kernel for the instances the
+    # pack kernel leaves) and a separate exchange kernel (sw_p2x_kernel; only
+    # batches that take the full kernel unfused launch it, so ~0 here)
     avg_plan_s = (ms_plan / max(runs, 1)) / 1e3
     avg_p2x_s = (ms_p2x / max(runs, 1)) / 1e3
     avg_kernel_s = avg_plan_s + avg_p2x_s
@@ -405,15 +407,16 @@ def main():
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": (f"{traffic[1]} (rocprofv3 PMC pass of this workload, "
                                    "FETCH_SIZE x2 + WRITE_SIZE)") if traffic else None,
-                "kernel": ("plan solve: sw_level_kernel + sw_pack_kernel + sw_plan_kernel (instances the "
-                           "pack kernel leaves) + sw_p2x_kernel, back to back on one stream"),
+                "kernel": ("plan solve: sw_level_kernel + sw_pack_kernel (pack, emit and the P2 exchange "
+                           "step per instance) + sw_plan_kernel (instances the pack kernel leaves), back "
+                           "to back on one stream"),
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "avg_kernel_ms_by_stage": {"plan": avg_plan_s * 1e3, "p2x": avg_p2x_s * 1e3},
                 "algorithmic_bytes_per_instance": algorithmic_bytes(args.jobs, args.rounds),
-                "limiter": ("not HBM: VALU issue (sw_level_kernel, sw_p2x_kernel: their VALU "
-                            "instructions at one wave64 instruction per CU per cycle are ~3/4 of "
-                            "their time) and the dependent block-phase chain of the pack kernel's "
-                            "one-wave round loop (DESIGN.md §6)"),
+                "limiter": ("not HBM: VALU issue in sw_level_kernel (its VALU instructions at one "
+                            "wave64 instruction per CU per cycle are ~3/4 of its time) and, in "
+                            "sw_pack_kernel, the dependent block-phase chains of the one-wave round "
+                            "loop and the exchange step's Bellman-Ford and edge builds (DESIGN.md §6)"),
                 "note": ("achieved = bytes a solve must move through HBM (inputs in; plan, counts, "
                          "result out) / the solve kernels' time — the HBM roof is the contract's "
                          "reference line, not the bound: the working sets stay in VGPRs/LDS "
