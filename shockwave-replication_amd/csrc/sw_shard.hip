@@ -931,6 +931,34 @@ int wave_pack_max() {
     return v;
 }
 
+/* The round loop for up to 8·NT active entries with E = 2, 4 or 8 positions
+ * per thread chosen by A at run time (one launch; the E = 8 body sets the
+ * registers, well inside the budget): the per-position loops of every pass
+ * walk what the entries need, not what M allows — a rank's share placement
+ * has M = its job count but A = its jobs with rounds (≈ 3/8 of them at C4). */
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pack_ent* all, int64_t M,
+                                                        const int32_t* order, uint64_t* ydst, int32_t* pdst,
+                                                        CapsArg caps, int alo, int zero) {
+    __shared__ sw_xchg_t<NT / 64> X;
+    __shared__ sw_pack_lds PL;
+    __shared__ int32_t capsL[64];
+    sw_blk_t<NT / 64> blk;
+    blk.X = &X;
+    blk.par = 0;
+    const int tid = threadIdx.x;
+    if (caps.has && tid < S.T) capsL[tid] = caps.v[tid];
+    int act = 0;
+    for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
+    const int A = blk.sum32(act); /* its barrier publishes capsL */
+    if (A <= alo || A > 8 * NT) return; /* another variant places these */
+    if (zero) /* a whole placement (not one width class): every row of this rank */
+        for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
+    if (A <= 2 * NT) pack_rounds_body<2>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    else if (A <= 4 * NT) pack_rounds_body<4>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    else pack_rounds_body<8>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+}
+
 /* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
 
 /* one gathered entry per job (the pack's gather buffer, reused) */
@@ -2019,24 +2047,25 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
         LAUNCH(S, k_pack_rounds_wave, dim3(1), dim3(64), 0, st, dv, all, M, S->porder.p, yd, pd, capsd, wa,
                (int)(mode != 5));
     const int lo = wave ? wa : -1;
+#define SW_LAUNCH_SEL(NT, ALO)                                                                  \
+    LAUNCH(S, (k_pack_rounds_sel<NT>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, pd, \
+           capsd, (int)(ALO), (int)(mode != 5))
+    /* measured on C4's share placement (profiles/r7nt1_*): E by the active
+     * entries in one launch against E by the entries, rank loop 148 → 125 µs
+     * at W = 2 and 122 → 90 µs at W = 4; 256-thread loops (4 waves, twice the
+     * positions per thread) were slower at W = 1 (0.729 against 0.706 ms) */
     if (wave && M <= wa) {
-    } else if (M <= 2 * SW_BLOCK) {
-        SW_LAUNCH_PACK(2, SW_BLOCK, lo);
-    } else if (M <= 8 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
-    } else if (M <= 20 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
-        SW_LAUNCH_PACK(20, SW_BLOCK, 8 * SW_BLOCK);
-    } else if (M <= 32 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
-        SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
     } else if (M <= 64 * SW_BLOCK) {
-        SW_LAUNCH_PACK(8, SW_BLOCK, lo);
-        SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
+        /* E by the active entries: one launch up to 8·512 of them */
+        SW_LAUNCH_SEL(SW_BLOCK, lo);
+        if (M > 32 * SW_BLOCK) SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
+        else if (M > 20 * SW_BLOCK) SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
+        else if (M > 8 * SW_BLOCK) SW_LAUNCH_PACK(20, SW_BLOCK, 8 * SW_BLOCK);
     } else {
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
     }
 #undef SW_LAUNCH_PACK
+#undef SW_LAUNCH_SEL
     return SW_OK;
 }
 
