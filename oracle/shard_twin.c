@@ -706,3 +706,8 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     for (int a = 0; a < SW_Y_COUNT; ++a) free(E.y[a]);
     return rc < 0 ? SW_ERR_RCCL : rc;
 }
+
+/* sw_share_caps (sw_shard_ctl.h) for tests/test_shard.py's property test. */
+int shard_share_caps(const int64_t* loads, int32_t W, int32_t rank, int32_t T, int64_t G, int32_t* caps) {
+    return sw_share_caps(loads, W, rank, T, G, caps);
+}

@@ -317,3 +317,59 @@ def test_share_p2_vs_milp_on_large_instances(world, shard_lib, twin):
         assert rs["p2_objective"] <= c["p2_milp"] * SHARE_P2_RATIO, \
             (c["N"], world, rs["p2_objective"] / c["p2_milp"])
         assert_share_contract(rs, twin.solve(a), f"N={c['N']} W={world}")
+
+
+def _share_caps_ref(loads, W, rank, T, G):
+    """sw_share_caps restated in exact integers."""
+    L = sum(loads)
+    C = G * T
+    if L <= 0 or L > C or T < 1:
+        return None
+    S = C - L
+    rest = S - sum(S * x // L for x in loads)
+    B = [loads[r] + S * loads[r] // L + (1 if r < rest else 0) for r in range(W)]
+    cursor = sum(b % T for b in B[:rank]) % T
+    base, ext = divmod(B[rank], T)
+    return [base + (1 if (t - cursor) % T < ext else 0) for t in range(T)], B[rank]
+
+
+def test_share_caps_properties(shard_lib):
+    """Every round's shares sum to G; rank r's shares sum to its budget
+    B_r ≥ its load and differ by at most one across rounds; world 1 is G in
+    every round; an empty or over-full load is refused."""
+    import ctypes
+
+    f = shard_lib.shard_share_caps
+    f.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                  ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]
+    f.restype = ctypes.c_int
+    rng = np.random.default_rng(7)
+
+    def caps_of(loads, W, r, T, G):
+        ld = np.ascontiguousarray(loads, dtype=np.int64)
+        out = np.zeros(T, dtype=np.int32)
+        rc = f(ld.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), W, r, T, G,
+               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return rc, out
+
+    for _ in range(300):
+        W = int(rng.choice([1, 2, 4, 8, 16]))
+        T = int(rng.integers(1, 65))
+        G = int(rng.integers(1, 5000))
+        loads = rng.integers(0, G * T // W + 1, size=W)
+        if loads.sum() == 0:
+            loads[0] = 1
+        rows = []
+        for r in range(W):
+            rc, caps = caps_of(loads, W, r, T, G)
+            ref = _share_caps_ref([int(x) for x in loads], W, r, T, G)
+            assert rc == 0 and ref is not None
+            assert caps.tolist() == ref[0], (W, r, T, G)
+            assert int(caps.sum()) == ref[1] >= int(loads[r])
+            assert caps.max() - caps.min() <= 1
+            rows.append(caps)
+        assert (np.sum(rows, axis=0) == G).all()
+        if W == 1:
+            assert (rows[0] == G).all()
+    assert caps_of([0, 0], 2, 0, 4, 10)[0] == -1
+    assert caps_of([30, 11], 2, 0, 4, 10)[0] == -1
