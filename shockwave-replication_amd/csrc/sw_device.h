@@ -19,7 +19,7 @@
 
 #include "sw_arith.h"
 
-#define SW_STAMP_SLOTS 48 /* per-instance u64 slots of the SW_STAMPS diagnostic build (32…47: sw_p2x_kernel) */
+#define SW_STAMP_SLOTS 64 /* per-instance u64 slots of the SW_STAMPS diagnostic build (32…42: sw_p2x_kernel, 48…52: pack sub-phases) */
 #define SW_LDS_JOBS 1024 /* instances up to this many jobs keep all state on chip (2 per thread) */
 
 struct sw_inst_dev {

@@ -1063,6 +1063,22 @@ struct Ctx {
     __device__ __forceinline__ void pack(int MODE, const uint8_t* nin, uint64_t* y,
                                          uint8_t* placed_out) {
         __syncthreads();
+#ifdef SW_STAMPS
+        /* pack sub-phases, thread 0's view: swp[40] keys and offsets, [41]
+         * compaction after the sort, [42] the round loop with its staging,
+         * [43] the row write-back (swp = stamps + 8: slots 48…51) */
+        uint64_t pk0_ = __builtin_amdgcn_s_memtime();
+#define PK_STAMP(k)                                                      \
+    do {                                                                 \
+        const uint64_t n_ = __builtin_amdgcn_s_memtime();                \
+        if (threadIdx.x == 0 && swp) swp[40 + (k)] += n_ - pk0_;         \
+        pk0_ = n_;                                                       \
+    } while (0)
+#else
+#define PK_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
         double Mb = 0.0;
         const int32_t* capsp = MODE == 5 ? caps : nullptr;
         if (MODE == 1 || MODE == 3) {
@@ -1085,6 +1101,7 @@ struct Ctx {
             int32_t A32;
             const int32_t abase = blk.exscan((int32_t)act_l, A32);
             const int A_ = A32;
+            PK_STAMP(0);
 #ifdef SW_STAMPS
             const uint64_t srt0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -1132,6 +1149,7 @@ struct Ctx {
                 }
 #ifdef SW_STAMPS
                 if (threadIdx.x == 0 && swp) swp[7] += __builtin_amdgcn_s_memtime() - srt0_;
+                pk0_ = __builtin_amdgcn_s_memtime();
 #endif
                 const int jp1 = !mine ? 0
                                 : ratio ? (int)(2047u - (uint32_t)(h1 & 2047u))
@@ -1139,6 +1157,7 @@ struct Ctx {
                 const uint32_t wq = MODE == 5 ? 1u : (uint32_t)w_in[jp1];
                 uint32_t st1[1] = {mine ? ((uint32_t)nin[jp1] | (wq << 8)) : 0u};
                 uint64_t mk1[1] = {0ull};
+                PK_STAMP(1);
                 /* the round loop in wave 0 (sw_pack_rounds_one; the sort is
                  * done with sbuf, whose first 6 KB stage the states): the
                  * pack kernel sizes it by A, the plan kernel takes the 6-
@@ -1149,6 +1168,7 @@ struct Ctx {
 #else
                 sw_pack_rounds_one<SMALL>(PL, A_, T, G, st1[0], mk1[0], sbuf, capsp);
 #endif
+                PK_STAMP(2);
                 for_jobs([&](int j, int s) {
                     (void)s;
                     if (owns(MODE, nin, j)) placed_out[j] = 0;
@@ -1159,6 +1179,7 @@ struct Ctx {
                     placed_out[jp1] = (uint8_t)(nin[jp1] - st_r(st1[0]));
                 }
                 __syncthreads();
+                PK_STAMP(3);
             } else {
                 if constexpr (!SMALL) {
                 if (ratio) sort_regs64(khi);
@@ -1238,6 +1259,7 @@ struct Ctx {
             }
             __syncthreads();
         }
+#undef PK_STAMP
     }
 
     /*
@@ -2015,6 +2037,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         uint8_t* pl = (mode == 3) ? c.placed2 : c.placed;
         uint64_t* yd = (mode == 3) ? c.y2 : c.ycur;
         c.pack(mode, c.nbest, yd, pl);
+#ifdef SW_STAMPS
+        const uint64_t ev0_ = __builtin_amdgcn_s_memtime();
+#endif
         int64_t def_l = 0;
         double fs = 0.0, gm = 0.0;
         c.for_jobs([&](int j, int s) {
@@ -2027,6 +2052,9 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
         c.blk.detsum_max(fs, gm, U, Mx);
         double Jo = U - c.k * Mx;
         c.passes++;
+#ifdef SW_STAMPS
+        if (threadIdx.x == 0 && c.swp) c.swp[44] += __builtin_amdgcn_s_memtime() - ev0_; /* slot 52 */
+#endif
         if (mode == 4) { /* density order: also the P2 placement when it packs */
             /* stranded rounds: repair the width profile (sw_repair.h) */
             if (dfc != 0 && c.repair_pack(c.nbest, c.ycur, c.placed, c.y2, c.placed2)) {

@@ -12,7 +12,7 @@ import sys
 
 import numpy as np
 
-SLOTS = 48  # SW_STAMP_SLOTS (csrc/sw_device.h)
+SLOTS = 64  # SW_STAMP_SLOTS (csrc/sw_device.h)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shockwave-replication_amd"))
@@ -65,6 +65,8 @@ def main():
             *st_all[:, 28:31].mean(axis=0), st_all[:, 31].mean() / max(rounds, 1)))
         print(f"   sorts (all packs): {srt.mean():.0f}; rounds {rounds:.1f}, active tiers {scans:.1f}, "
               f"width-tail reductions {misses:.1f}")
+        print("   pack sub-phases (all packs): keys+offsets {:.0f} compaction {:.0f} loop+staging {:.0f} "
+              "write-back {:.0f} | post-pack evaluation {:.0f}".format(*st_all[:, 48:53].mean(axis=0)))
         lnames = ["force", "price_probes", "tie", "tail", "eval", "M_lo", "between"]
         print("   level search:", " ".join(f"{n} {ls[:, i].mean():.0f}" for i, n in enumerate(lnames)),
               f"| price probes {st_all[:, 23].mean():.1f}, M_lo passes {st_all[:, 24].mean():.1f}")
