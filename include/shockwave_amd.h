@@ -305,6 +305,32 @@ int sw_mmf_allocate(sw_handle* h, int32_t num_jobs, int32_t num_workers,
                     const int32_t* scale_factors, const double* coefficients, double* allocation,
                     double* level);
 
+/*
+ * The heterogeneity-aware allocation over several worker types:
+ * MaxMinFairnessPolicyWithPerf.get_allocation (policies/max_min_fairness.py:
+ * 44-100) with the base constraints of policy.py:57-63,
+ *
+ *     maximise min_j Σ_k coefficients[j][k]·x[j][k]
+ *     s.t.  Σ_j scale_factors[j]·x[j][k] ≤ workers[k]  (every type k),
+ *           Σ_k x[j][k] ≤ 1,  x ≥ 0,
+ *
+ * coefficients row-major [num_jobs][num_types] = throughput · priority weight
+ * · scale factor (the caller's normalisation, max_min_fairness.py:57-73; the
+ * Fig-9 policy, MaxMinFairnessPolicy, passes unit throughputs), jobs in sorted
+ * id order, types in sorted name order (policy.py:28-44).  Solved exactly by
+ * the simplex method (Bland's rule) on the GPU: allocation receives an
+ * optimal vertex (row-major, unclipped), level[0] the optimal min share t*,
+ * level[1] the pivots taken.  ECOS, the reference's solver, returns an
+ * interior point of the same optimal face: the level is the LP's, the
+ * allocation is one of its optima (the same one only where it is unique).
+ * Limits: num_jobs ≤ 2048, 1 ≤ num_types ≤ 16, tableau ≤ 256 MB
+ * (SW_ERR_CAPACITY).  Synchronous; num_jobs = 0 is a no-op.  Added in
+ * round 5; reference interface: the WithPerf policy's get_allocation.
+ */
+int sw_mmf_allocate_types(sw_handle* h, int32_t num_jobs, int32_t num_types, const int32_t* workers,
+                          const int32_t* scale_factors, const double* coefficients, double* allocation,
+                          double* level);
+
 #ifdef __cplusplus
 }
 #endif

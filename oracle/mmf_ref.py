@@ -72,3 +72,56 @@ def twin_allocate(scale_factors, coefficients, num_workers):
 def twin_allocator(scale_factors, coefficients, num_workers):
     """The simulator's allocator interface backed by the twin."""
     return twin_allocate(scale_factors, coefficients, num_workers)[0]
+
+
+def lp_level_types(workers, scale_factors, coefficients):
+    """The heterogeneity-aware LP (policies/max_min_fairness.py:44-100 with
+    policy.py:57-63), m jobs × n types, solved by HiGHS: max t s.t.
+    t ≤ Σ_k coef[j][k]·x[j][k], Σ_j sf_j·x[j][k] ≤ workers[k], Σ_k x[j][k] ≤ 1,
+    x ≥ 0.  Returns (t*, x[m][n])."""
+    W = np.asarray(workers, dtype=np.float64)
+    sf = np.asarray(scale_factors, dtype=np.float64)
+    c = np.asarray(coefficients, dtype=np.float64)
+    m, n = c.shape
+    nv = m * n + 1
+    obj = np.zeros(nv)
+    obj[-1] = -1.0
+    rows, b = [], []
+    for j in range(m):
+        r = np.zeros(nv)
+        r[j * n:(j + 1) * n] = -c[j]
+        r[-1] = 1.0
+        rows.append(r)
+        b.append(0.0)
+    for k in range(n):
+        r = np.zeros(nv)
+        r[k:m * n:n] = sf
+        rows.append(r)
+        b.append(W[k])
+    for j in range(m):
+        r = np.zeros(nv)
+        r[j * n:(j + 1) * n] = 1.0
+        rows.append(r)
+        b.append(1.0)
+    res = linprog(obj, A_ub=np.array(rows), b_ub=np.array(b), bounds=[(0.0, None)] * nv, method="highs")
+    assert res.status == 0, res.message
+    return -res.fun, res.x[:m * n].reshape(m, n)
+
+
+def twin_allocate_types(workers, scale_factors, coefficients):
+    """(x[m][n], t*, pivots) from the CPU twin of the simplex kernel."""
+    W = np.ascontiguousarray(workers, dtype=np.int32)
+    sf = np.ascontiguousarray(scale_factors, dtype=np.int32)
+    c = np.ascontiguousarray(coefficients, dtype=np.float64)
+    m, n = c.shape
+    x = np.zeros(m * n)
+    lvl = np.zeros(2)
+    piv = C.c_int64()
+    lib = _lib()
+    dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+    lib.mmf_twin_allocate_types.argtypes = [C.c_int32, C.c_int32, ip, ip, dp, dp, dp, C.POINTER(C.c_int64)]
+    lib.mmf_twin_allocate_types.restype = C.c_int
+    rc = lib.mmf_twin_allocate_types(m, n, W.ctypes.data_as(ip), sf.ctypes.data_as(ip), c.ctypes.data_as(dp),
+                                     x.ctypes.data_as(dp), lvl.ctypes.data_as(dp), C.byref(piv))
+    assert rc == 0, rc
+    return x.reshape(m, n), float(lvl[0]), int(piv.value)

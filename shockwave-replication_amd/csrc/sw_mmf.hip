@@ -27,6 +27,7 @@
 #include "sw_block.h"
 #include "sw_handle.h"
 #include "sw_mmf.h"
+#include "sw_mmf_lp.h"
 
 namespace {
 
@@ -83,11 +84,125 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_mmf_kernel(int32_t N, int32_t G,
     if (threadIdx.x == 0) { out[0] = t; out[1] = mu; }
 }
 
+/*
+ * The heterogeneity-aware LP over worker types (sw_mmf_lp.h): the primal
+ * simplex on a dense tableau in HBM (L2-resident at Gavel sizes: 200 jobs ×
+ * 3 types is 3.2 MB), one 512-thread workgroup.  Per pivot: the entering
+ * column (first negative objective entry: a block min over column stripes),
+ * the leaving row (least ratio, then least basic index: a wave butterfly and
+ * an eight-way combine), the entering column's entries saved to LDS, the
+ * pivot row divided, then every other row with a nonzero factor updated by
+ * one wave (lanes over columns, coalesced).  The pivots and every element's
+ * arithmetic are oracle/mmf_twin.c's, so the tableau's bits are the twin's.
+ * LDS: the factors (R + 1 doubles) and the basis (R ints).
+ */
+struct LpKey {
+    double r;
+    int32_t b, i;
+};
+
+__device__ __forceinline__ void lp_take(LpKey& k, const LpKey& o) {
+    if (o.i >= 0 && (k.i < 0 || sw_lp_before(o.r, o.b, k.r, k.b))) k = o;
+}
+
+__global__ __launch_bounds__(SW_BLOCK) void sw_mmf_lp_kernel(int32_t m, int32_t n, const int32_t* workers,
+                                                             const int32_t* sf, const double* coef,
+                                                             double* a, double* x, double* out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lp_smem[];
+    __shared__ sw_xchg X;
+    __shared__ LpKey wk[SW_WAVES];
+    __shared__ int32_t sr;
+    sw_blk blk{&X, 0};
+    const sw_lp_dims d = sw_lp_dims_of(m, n);
+    const int64_t W = d.W, R1 = (int64_t)d.R + 1;
+    double* f = reinterpret_cast<double*>(lp_smem);
+    int32_t* basis = reinterpret_cast<int32_t*>(lp_smem + ((R1 * 8 + 15) & ~(int64_t)15));
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    for (int64_t e = tid; e < R1 * W; e += SW_BLOCK)
+        a[e] = sw_lp_init(&d, workers, sf, coef, (int32_t)(e / W), (int32_t)(e % W));
+    for (int32_t i = tid; i < d.R; i += SW_BLOCK) basis[i] = m * n + 1 + i;
+    __syncthreads();
+    const double* obj = a + (int64_t)d.R * W;
+    const int64_t maxp = sw_lp_max_pivots(&d);
+    int64_t piv = 0;
+    int32_t status = 0;
+    for (;;) {
+        int32_t el = 0x7FFFFFFF;
+        for (int32_t c = tid; c < d.C; c += SW_BLOCK)
+            if (obj[c] < -SW_LP_EPS) { el = c; break; }
+        const int32_t e = blk.min32(el);
+        if (e == 0x7FFFFFFF) break; /* optimal (uniform) */
+        LpKey k;
+        k.r = 0.0; k.b = 0; k.i = -1;
+        for (int32_t i = tid; i < d.R; i += SW_BLOCK) {
+            const double v = a[(int64_t)i * W + e];
+            if (v > SW_LP_EPS) {
+                LpKey o;
+                o.r = a[(int64_t)i * W + d.C] / v;
+                o.b = basis[i];
+                o.i = i;
+                lp_take(k, o);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            LpKey o;
+            o.r = __shfl_xor(k.r, off, 64);
+            o.b = __shfl_xor(k.b, off, 64);
+            o.i = __shfl_xor(k.i, off, 64);
+            lp_take(k, o);
+        }
+        if (lane == 0) wk[wv] = k;
+        __syncthreads();
+        if (tid == 0) {
+            LpKey kk = wk[0];
+            for (int w = 1; w < SW_WAVES; ++w) lp_take(kk, wk[w]);
+            sr = kk.i;
+        }
+        __syncthreads();
+        const int32_t r = sr;
+        if (r < 0) { status = -2; break; }
+        if (++piv > maxp) { status = -3; break; }
+        for (int64_t i = tid; i < R1; i += SW_BLOCK) f[i] = a[i * W + e];
+        __syncthreads();
+        const double pe = f[r];
+        double* pr = a + (int64_t)r * W;
+        for (int64_t c = tid; c < W; c += SW_BLOCK) pr[c] = pr[c] / pe;
+        __syncthreads();
+        for (int64_t i = wv; i < R1; i += SW_WAVES) {
+            const double fi = f[i];
+            if (i == r || fi == 0.0) continue;
+            double* ai = a + i * W;
+            for (int64_t c = lane; c < W; c += 64) ai[c] = ai[c] - fi * pr[c];
+        }
+        __syncthreads();
+        if (tid == 0) basis[r] = e;
+        __syncthreads();
+    }
+    for (int32_t j = tid; j < m * n; j += SW_BLOCK) x[j] = 0.0;
+    __syncthreads();
+    for (int32_t i = tid; i < d.R; i += SW_BLOCK) {
+        const int32_t b = basis[i];
+        const double v = a[(int64_t)i * W + d.C];
+        if (b < m * n) x[b] = v;
+        else if (b == m * n) out[0] = v;
+    }
+    if (tid == 0) {
+        out[1] = (double)piv;
+        out[2] = (double)status;
+    }
+}
+
 struct MmfBufs {
     DevBuf<int32_t> sf;
     DevBuf<double> c, x, out;
     HostBuf<int32_t> hsf;
     HostBuf<double> hc, hx, hout;
+    /* the LP over worker types */
+    DevBuf<int32_t> lw, lsf;
+    DevBuf<double> lc, lx, lout, tab;
+    HostBuf<int32_t> hlw, hlsf;
+    HostBuf<double> hlc, hlx, hlout;
 };
 
 int mmf_fail(sw_handle* h, int code, const std::string& msg) {
@@ -109,6 +224,8 @@ void sw_mmf_release(sw_handle* h) {
     MmfBufs* b = (MmfBufs*)h->mmf;
     b->sf.release(); b->c.release(); b->x.release(); b->out.release();
     b->hsf.release(); b->hc.release(); b->hx.release(); b->hout.release();
+    b->lw.release(); b->lsf.release(); b->lc.release(); b->lx.release(); b->lout.release(); b->tab.release();
+    b->hlw.release(); b->hlsf.release(); b->hlc.release(); b->hlx.release(); b->hlout.release();
     delete b;
     h->mmf = nullptr;
 }
@@ -157,5 +274,70 @@ extern "C" int sw_mmf_allocate(sw_handle* h, int32_t num_jobs, int32_t num_worke
     MMF_HIP(h, hipStreamSynchronize(h->stream));
     memcpy(allocation, b->hx.p, n * sizeof(double));
     if (level) { level[0] = b->hout.p[0]; level[1] = b->hout.p[1]; }
+    return SW_OK;
+}
+
+extern "C" int sw_mmf_allocate_types(sw_handle* h, int32_t num_jobs, int32_t num_types,
+                                     const int32_t* workers, const int32_t* scale_factors,
+                                     const double* coefficients, double* allocation, double* level) {
+    if (!h) return SW_ERR_INVALID;
+    if (num_jobs < 0 || num_jobs > SW_LP_MAX_JOBS || num_types < 1 || num_types > SW_LP_MAX_TYPES ||
+        !workers || (num_jobs > 0 && (!scale_factors || !coefficients || !allocation)))
+        return mmf_fail(h, SW_ERR_INVALID, "sw_mmf_allocate_types: bad sizes or null pointers");
+    for (int32_t k = 0; k < num_types; ++k)
+        if (workers[k] < 0)
+            return mmf_fail(h, SW_ERR_INVALID, "sw_mmf_allocate_types: worker counts must be >= 0");
+    for (int32_t j = 0; j < num_jobs; ++j) {
+        if (scale_factors[j] < 1 || scale_factors[j] > SW_MAX_WIDTH)
+            return mmf_fail(h, SW_ERR_INVALID, "sw_mmf_allocate_types: scale factors must be in [1,255]");
+        for (int32_t k = 0; k < num_types; ++k) {
+            const double c = coefficients[(size_t)j * num_types + k];
+            if (!(c >= 0.0) || !isfinite(c))
+                return mmf_fail(h, SW_ERR_INVALID,
+                                "sw_mmf_allocate_types: coefficients must be finite and >= 0");
+        }
+    }
+    if (level) { level[0] = 0.0; level[1] = 0.0; }
+    if (num_jobs == 0) return SW_OK; /* policy.flatten returns None (policy.py:28-33) */
+    const sw_lp_dims d = sw_lp_dims_of(num_jobs, num_types);
+    const size_t cells = (size_t)(d.R + 1) * (size_t)d.W;
+    if (cells * sizeof(double) > ((size_t)1 << 28))
+        return mmf_fail(h, SW_ERR_CAPACITY, "sw_mmf_allocate_types: tableau above 256 MB");
+    const size_t lds = (((size_t)(d.R + 1) * 8 + 15) & ~(size_t)15) + (size_t)d.R * 4;
+    MMF_HIP(h, hipSetDevice(h->device));
+    if (!h->mmf) h->mmf = new MmfBufs();
+    MmfBufs* b = (MmfBufs*)h->mmf;
+    const size_t m = (size_t)num_jobs, mn = m * (size_t)num_types;
+    MMF_HIP(h, b->lw.reserve((size_t)num_types));
+    MMF_HIP(h, b->lsf.reserve(m));
+    MMF_HIP(h, b->lc.reserve(mn));
+    MMF_HIP(h, b->lx.reserve(mn));
+    MMF_HIP(h, b->lout.reserve(4));
+    MMF_HIP(h, b->tab.reserve(cells));
+    MMF_HIP(h, b->hlw.reserve((size_t)num_types));
+    MMF_HIP(h, b->hlsf.reserve(m));
+    MMF_HIP(h, b->hlc.reserve(mn));
+    MMF_HIP(h, b->hlx.reserve(mn));
+    MMF_HIP(h, b->hlout.reserve(4));
+    memcpy(b->hlw.p, workers, (size_t)num_types * sizeof(int32_t));
+    memcpy(b->hlsf.p, scale_factors, m * sizeof(int32_t));
+    memcpy(b->hlc.p, coefficients, mn * sizeof(double));
+    hipStream_t st = h->stream;
+    MMF_HIP(h, hipMemcpyAsync(b->lw.p, b->hlw.p, (size_t)num_types * 4, hipMemcpyHostToDevice, st));
+    MMF_HIP(h, hipMemcpyAsync(b->lsf.p, b->hlsf.p, m * 4, hipMemcpyHostToDevice, st));
+    MMF_HIP(h, hipMemcpyAsync(b->lc.p, b->hlc.p, mn * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(sw_mmf_lp_kernel, dim3(1), dim3(SW_BLOCK), lds, st, num_jobs, num_types, b->lw.p, b->lsf.p,
+                       b->lc.p, b->tab.p, b->lx.p, b->lout.p);
+    MMF_HIP(h, hipGetLastError());
+    MMF_HIP(h, hipMemcpyAsync(b->hlx.p, b->lx.p, mn * 8, hipMemcpyDeviceToHost, st));
+    MMF_HIP(h, hipMemcpyAsync(b->hlout.p, b->lout.p, 3 * 8, hipMemcpyDeviceToHost, st));
+    MMF_HIP(h, hipStreamSynchronize(st));
+    const int status = (int)b->hlout.p[2];
+    if (status != 0)
+        return mmf_fail(h, SW_ERR_CAPACITY,
+                        status == -3 ? "sw_mmf_allocate_types: pivot cap reached"
+                                     : "sw_mmf_allocate_types: no leaving row (unbounded)");
+    memcpy(allocation, b->hlx.p, mn * sizeof(double));
+    if (level) { level[0] = b->hlout.p[0]; level[1] = b->hlout.p[1]; }
     return SW_OK;
 }

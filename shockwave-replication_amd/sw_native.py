@@ -317,6 +317,7 @@ EXPORTED_SYMBOLS = (
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
     "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
     "sw_dist_init_host", "sw_mmf_allocate", "sw_dist_plan_solve_dev", "sw_dist_enable_peer",
+    "sw_mmf_allocate_types",
 )
 
 
@@ -388,6 +389,8 @@ def load(path: str | None = None):
     lib.sw_dist_enable_peer.restype = C.c_int
     lib.sw_mmf_allocate.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _ip, _dp, _dp, _dp]
     lib.sw_mmf_allocate.restype = C.c_int
+    lib.sw_mmf_allocate_types.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _ip, _ip, _dp, _dp, _dp]
+    lib.sw_mmf_allocate_types.restype = C.c_int
     if path is None:
         _LIB = lib
     return lib
@@ -496,6 +499,22 @@ class Solver:
                                              x.ctypes.data_as(_dp), lvl.ctypes.data_as(_dp)),
                     "sw_mmf_allocate")
         return x, float(lvl[0]), float(lvl[1])
+
+    def mmf_allocate_types(self, workers, scale_factors, coefficients):
+        """x[j][k] of the heterogeneity-aware MaxMinFairness LP over worker
+        types (sw_mmf_allocate_types); returns (x [m, n], t*, pivots)."""
+        w = np.ascontiguousarray(workers, dtype=np.int32)
+        sf = np.ascontiguousarray(scale_factors, dtype=np.int32)
+        c = np.ascontiguousarray(coefficients, dtype=np.float64)
+        if c.ndim != 2 or c.shape != (len(sf), len(w)):
+            raise ValueError("coefficients must be [num_jobs][num_types]")
+        x = np.zeros(c.shape, dtype=np.float64)
+        lvl = np.zeros(2, dtype=np.float64)
+        self._check(self.lib.sw_mmf_allocate_types(self.h, c.shape[0], c.shape[1], w.ctypes.data_as(_ip),
+                                                   sf.ctypes.data_as(_ip), c.ctypes.data_as(_dp),
+                                                   x.ctypes.data_as(_dp), lvl.ctypes.data_as(_dp)),
+                    "sw_mmf_allocate_types")
+        return x, float(lvl[0]), int(lvl[1])
 
     # ---- sharded single instance (include/shockwave_amd.h sw_dist_*) ----
     def dist_init(self, unique_id: bytes, rank: int, world: int):
