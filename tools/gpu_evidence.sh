@@ -25,7 +25,8 @@ timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_peer4 -o run_%pid% -- python3 tools/peer_timing.py 4 40 > $OUT/prof_peer4.log 2>&1 &&
 timeout -k 10 120 python -u tools/boundary.py > $OUT/boundary.json 2> $OUT/boundary.err &&
 timeout -k 10 120 python -u tools/c5_stages.py > $OUT/c5_stages.json 2> $OUT/c5_stages.err &&
-timeout -k 10 200 python -u tools/stamps.py --c5 > $OUT/stamps_c5.log 2>&1
+timeout -k 10 200 python -u tools/stamps.py --c5 > $OUT/stamps_c5.log 2>&1 &&
+timeout -k 10 120 python -u tools/mmf_types_timing.py > $OUT/mmf_types_timing.json 2> $OUT/mmf_types_timing.err
 rc=$?
 echo "exit $rc"; tail -2 $OUT/pytest_gpu.log; tail -1 $OUT/smoke.log; cat $OUT/bench.json; head -14 $OUT/stamps.log
 exit $rc
