@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 
 #include "../../include/shockwave_amd.h"
@@ -87,14 +88,22 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_mmf_kernel(int32_t N, int32_t G,
 /*
  * The heterogeneity-aware LP over worker types (sw_mmf_lp.h): the primal
  * simplex on a dense tableau in HBM (L2-resident at Gavel sizes: 200 jobs ×
- * 3 types is 3.2 MB), one 512-thread workgroup.  Per pivot: the entering
- * column (first negative objective entry: a block min over column stripes),
- * the leaving row (least ratio, then least basic index: a wave butterfly and
- * an eight-way combine), the entering column's entries saved to LDS, the
- * pivot row divided, then every other row with a nonzero factor updated by
- * one wave (lanes over columns, coalesced).  The pivots and every element's
- * arithmetic are oracle/mmf_twin.c's, so the tableau's bits are the twin's.
- * LDS: the factors (R + 1 doubles) and the basis (R ints).
+ * 3 types is 3.2 MB).  A pivot is a rank-one update of the whole tableau, so
+ * it runs on the whole GPU as two kernels chained on the stream, with the
+ * simplex state in device memory and no host round trip per pivot:
+ *   k_lp_select  (one workgroup) the entering column (first negative
+ *                objective entry: a block min over column stripes), the
+ *                leaving row (least ratio, then least basic index: a wave
+ *                butterfly and an eight-way combine), the entering column's
+ *                entries f_i and the divided pivot row p_j into buffers, the
+ *                basis update; sets the done flag at the optimum;
+ *   k_lp_update  (a workgroup per row) a_ij − f_i·p_j, the pivot row := p
+ *                (rows with f_i = 0 are skipped).
+ * The host enqueues pivots in chunks and reads the flag between chunks.  The
+ * pivots and every element's arithmetic are oracle/mmf_twin.c's, so the
+ * tableau's bits are the twin's.  (A first single-workgroup form, rows
+ * updated by its eight waves, took 45 ms at 200 jobs × 3 types — 124 µs per
+ * pivot of L2 latency — profiles/r7f_mmf_types_timing.json.)
  */
 struct LpKey {
     double r;
@@ -105,81 +114,111 @@ __device__ __forceinline__ void lp_take(LpKey& k, const LpKey& o) {
     if (o.i >= 0 && (k.i < 0 || sw_lp_before(o.r, o.b, k.r, k.b))) k = o;
 }
 
-__global__ __launch_bounds__(SW_BLOCK) void sw_mmf_lp_kernel(int32_t m, int32_t n, const int32_t* workers,
-                                                             const int32_t* sf, const double* coef,
-                                                             double* a, double* x, double* out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lp_smem[];
+/* simplex state in device memory: [0] done (0 running, 1 optimal, -2 no
+ * leaving row, -3 pivot cap), [1] pivots, [2] pivot row r, [3] entering e */
+struct LpState {
+    int64_t done, piv, r, e;
+};
+
+constexpr int kLpTB = 256;
+
+__global__ __launch_bounds__(kLpTB) void k_lp_init(int32_t m, int32_t n, const int32_t* workers, const int32_t* sf,
+                                                   const double* coef, double* a, int32_t* basis, LpState* st) {
+    const sw_lp_dims d = sw_lp_dims_of(m, n);
+    const int64_t W = d.W, cells = ((int64_t)d.R + 1) * W;
+    const int64_t g = (int64_t)blockIdx.x * kLpTB + threadIdx.x, stride = (int64_t)gridDim.x * kLpTB;
+    for (int64_t e = g; e < cells; e += stride) a[e] = sw_lp_init(&d, workers, sf, coef, (int32_t)(e / W), (int32_t)(e % W));
+    for (int64_t i = g; i < d.R; i += stride) basis[i] = m * n + 1 + (int32_t)i;
+    if (g == 0) { st->done = 0; st->piv = 0; st->r = -1; st->e = -1; }
+}
+
+__global__ __launch_bounds__(SW_BLOCK) void k_lp_select(int32_t m, int32_t n, const double* a, int32_t* basis,
+                                                        double* f, double* p, LpState* st) {
     __shared__ sw_xchg X;
     __shared__ LpKey wk[SW_WAVES];
     __shared__ int32_t sr;
+    if (st->done != 0) return; /* uniform: the optimum (or a stop) was reached */
+    const int64_t piv0 = st->piv; /* read once: thread 0 advances it below */
     sw_blk blk{&X, 0};
     const sw_lp_dims d = sw_lp_dims_of(m, n);
     const int64_t W = d.W, R1 = (int64_t)d.R + 1;
-    double* f = reinterpret_cast<double*>(lp_smem);
-    int32_t* basis = reinterpret_cast<int32_t*>(lp_smem + ((R1 * 8 + 15) & ~(int64_t)15));
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    for (int64_t e = tid; e < R1 * W; e += SW_BLOCK)
-        a[e] = sw_lp_init(&d, workers, sf, coef, (int32_t)(e / W), (int32_t)(e % W));
-    for (int32_t i = tid; i < d.R; i += SW_BLOCK) basis[i] = m * n + 1 + i;
-    __syncthreads();
     const double* obj = a + (int64_t)d.R * W;
-    const int64_t maxp = sw_lp_max_pivots(&d);
-    int64_t piv = 0;
-    int32_t status = 0;
-    for (;;) {
-        int32_t el = 0x7FFFFFFF;
-        for (int32_t c = tid; c < d.C; c += SW_BLOCK)
-            if (obj[c] < -SW_LP_EPS) { el = c; break; }
-        const int32_t e = blk.min32(el);
-        if (e == 0x7FFFFFFF) break; /* optimal (uniform) */
-        LpKey k;
-        k.r = 0.0; k.b = 0; k.i = -1;
-        for (int32_t i = tid; i < d.R; i += SW_BLOCK) {
-            const double v = a[(int64_t)i * W + e];
-            if (v > SW_LP_EPS) {
-                LpKey o;
-                o.r = a[(int64_t)i * W + d.C] / v;
-                o.b = basis[i];
-                o.i = i;
-                lp_take(k, o);
-            }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
+    int32_t el = 0x7FFFFFFF;
+    for (int32_t c = tid; c < d.C; c += SW_BLOCK)
+        if (obj[c] < -SW_LP_EPS) { el = c; break; }
+    const int32_t e = blk.min32(el);
+    if (e == 0x7FFFFFFF) {
+        if (tid == 0) st->done = 1;
+        return;
+    }
+    LpKey k;
+    k.r = 0.0; k.b = 0; k.i = -1;
+    for (int32_t i = tid; i < d.R; i += SW_BLOCK) {
+        const double v = a[(int64_t)i * W + e];
+        if (v > SW_LP_EPS) {
             LpKey o;
-            o.r = __shfl_xor(k.r, off, 64);
-            o.b = __shfl_xor(k.b, off, 64);
-            o.i = __shfl_xor(k.i, off, 64);
+            o.r = a[(int64_t)i * W + d.C] / v;
+            o.b = basis[i];
+            o.i = i;
             lp_take(k, o);
         }
-        if (lane == 0) wk[wv] = k;
-        __syncthreads();
-        if (tid == 0) {
-            LpKey kk = wk[0];
-            for (int w = 1; w < SW_WAVES; ++w) lp_take(kk, wk[w]);
-            sr = kk.i;
-        }
-        __syncthreads();
-        const int32_t r = sr;
-        if (r < 0) { status = -2; break; }
-        if (++piv > maxp) { status = -3; break; }
-        for (int64_t i = tid; i < R1; i += SW_BLOCK) f[i] = a[i * W + e];
-        __syncthreads();
-        const double pe = f[r];
-        double* pr = a + (int64_t)r * W;
-        for (int64_t c = tid; c < W; c += SW_BLOCK) pr[c] = pr[c] / pe;
-        __syncthreads();
-        for (int64_t i = wv; i < R1; i += SW_WAVES) {
-            const double fi = f[i];
-            if (i == r || fi == 0.0) continue;
-            double* ai = a + i * W;
-            for (int64_t c = lane; c < W; c += 64) ai[c] = ai[c] - fi * pr[c];
-        }
-        __syncthreads();
-        if (tid == 0) basis[r] = e;
-        __syncthreads();
     }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        LpKey o;
+        o.r = __shfl_xor(k.r, off, 64);
+        o.b = __shfl_xor(k.b, off, 64);
+        o.i = __shfl_xor(k.i, off, 64);
+        lp_take(k, o);
+    }
+    if (lane == 0) wk[wv] = k;
+    __syncthreads();
+    if (tid == 0) {
+        LpKey kk = wk[0];
+        for (int w = 1; w < SW_WAVES; ++w) lp_take(kk, wk[w]);
+        sr = kk.i;
+    }
+    __syncthreads();
+    const int32_t r = sr;
+    if (r < 0 || piv0 + 1 > sw_lp_max_pivots(&d)) {
+        if (tid == 0) st->done = r < 0 ? -2 : -3;
+        return;
+    }
+    for (int64_t i = tid; i < R1; i += SW_BLOCK) f[i] = a[i * W + e];
+    const double pe = a[(int64_t)r * W + e];
+    for (int64_t c = tid; c < W; c += SW_BLOCK) p[c] = a[(int64_t)r * W + c] / pe;
+    if (tid == 0) {
+        basis[r] = e;
+        st->piv = piv0 + 1;
+        st->r = r;
+        st->e = e;
+    }
+}
+
+__global__ __launch_bounds__(kLpTB) void k_lp_update(int32_t m, int32_t n, double* a, const double* f, const double* p,
+                                                     const LpState* st) {
+    if (st->done != 0) return;
+    const sw_lp_dims d = sw_lp_dims_of(m, n);
+    const int64_t W = d.W, i = blockIdx.x;
+    const int64_t r = st->r;
+    double* ai = a + i * W;
+    if (i == r) {
+        for (int64_t c = threadIdx.x; c < W; c += kLpTB) ai[c] = p[c];
+        return;
+    }
+    const double fi = f[i];
+    if (fi == 0.0) return;
+    for (int64_t c = threadIdx.x; c < W; c += kLpTB) ai[c] = ai[c] - fi * p[c];
+}
+
+__global__ __launch_bounds__(SW_BLOCK) void k_lp_result(int32_t m, int32_t n, const double* a, const int32_t* basis,
+                                                        const LpState* st, double* x, double* out) {
+    const sw_lp_dims d = sw_lp_dims_of(m, n);
+    const int64_t W = d.W;
+    const int tid = threadIdx.x;
     for (int32_t j = tid; j < m * n; j += SW_BLOCK) x[j] = 0.0;
+    if (tid == 0) out[0] = 0.0;
     __syncthreads();
     for (int32_t i = tid; i < d.R; i += SW_BLOCK) {
         const int32_t b = basis[i];
@@ -188,8 +227,8 @@ __global__ __launch_bounds__(SW_BLOCK) void sw_mmf_lp_kernel(int32_t m, int32_t 
         else if (b == m * n) out[0] = v;
     }
     if (tid == 0) {
-        out[1] = (double)piv;
-        out[2] = (double)status;
+        out[1] = (double)st->piv;
+        out[2] = (double)(st->done == 1 ? 0 : st->done);
     }
 }
 
@@ -199,8 +238,10 @@ struct MmfBufs {
     HostBuf<int32_t> hsf;
     HostBuf<double> hc, hx, hout;
     /* the LP over worker types */
-    DevBuf<int32_t> lw, lsf;
-    DevBuf<double> lc, lx, lout, tab;
+    DevBuf<int32_t> lw, lsf, lbasis;
+    DevBuf<double> lc, lx, lout, tab, lf, lp;
+    DevBuf<LpState> lst;
+    HostBuf<LpState> hlst;
     HostBuf<int32_t> hlw, hlsf;
     HostBuf<double> hlc, hlx, hlout;
 };
@@ -225,6 +266,7 @@ void sw_mmf_release(sw_handle* h) {
     b->sf.release(); b->c.release(); b->x.release(); b->out.release();
     b->hsf.release(); b->hc.release(); b->hx.release(); b->hout.release();
     b->lw.release(); b->lsf.release(); b->lc.release(); b->lx.release(); b->lout.release(); b->tab.release();
+    b->lbasis.release(); b->lf.release(); b->lp.release(); b->lst.release(); b->hlst.release();
     b->hlw.release(); b->hlsf.release(); b->hlc.release(); b->hlx.release(); b->hlout.release();
     delete b;
     h->mmf = nullptr;
@@ -303,7 +345,6 @@ extern "C" int sw_mmf_allocate_types(sw_handle* h, int32_t num_jobs, int32_t num
     const size_t cells = (size_t)(d.R + 1) * (size_t)d.W;
     if (cells * sizeof(double) > ((size_t)1 << 28))
         return mmf_fail(h, SW_ERR_CAPACITY, "sw_mmf_allocate_types: tableau above 256 MB");
-    const size_t lds = (((size_t)(d.R + 1) * 8 + 15) & ~(size_t)15) + (size_t)d.R * 4;
     MMF_HIP(h, hipSetDevice(h->device));
     if (!h->mmf) h->mmf = new MmfBufs();
     MmfBufs* b = (MmfBufs*)h->mmf;
@@ -314,6 +355,11 @@ extern "C" int sw_mmf_allocate_types(sw_handle* h, int32_t num_jobs, int32_t num
     MMF_HIP(h, b->lx.reserve(mn));
     MMF_HIP(h, b->lout.reserve(4));
     MMF_HIP(h, b->tab.reserve(cells));
+    MMF_HIP(h, b->lbasis.reserve((size_t)d.R));
+    MMF_HIP(h, b->lf.reserve((size_t)d.R + 1));
+    MMF_HIP(h, b->lp.reserve((size_t)d.W));
+    MMF_HIP(h, b->lst.reserve(1));
+    MMF_HIP(h, b->hlst.reserve(1));
     MMF_HIP(h, b->hlw.reserve((size_t)num_types));
     MMF_HIP(h, b->hlsf.reserve(m));
     MMF_HIP(h, b->hlc.reserve(mn));
@@ -326,8 +372,27 @@ extern "C" int sw_mmf_allocate_types(sw_handle* h, int32_t num_jobs, int32_t num
     MMF_HIP(h, hipMemcpyAsync(b->lw.p, b->hlw.p, (size_t)num_types * 4, hipMemcpyHostToDevice, st));
     MMF_HIP(h, hipMemcpyAsync(b->lsf.p, b->hlsf.p, m * 4, hipMemcpyHostToDevice, st));
     MMF_HIP(h, hipMemcpyAsync(b->lc.p, b->hlc.p, mn * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(sw_mmf_lp_kernel, dim3(1), dim3(SW_BLOCK), lds, st, num_jobs, num_types, b->lw.p, b->lsf.p,
-                       b->lc.p, b->tab.p, b->lx.p, b->lout.p);
+    const unsigned gi = (unsigned)std::min<size_t>((cells + kLpTB - 1) / kLpTB, 4096);
+    hipLaunchKernelGGL(k_lp_init, dim3(gi), dim3(kLpTB), 0, st, num_jobs, num_types, b->lw.p, b->lsf.p, b->lc.p,
+                       b->tab.p, b->lbasis.p, b->lst.p);
+    MMF_HIP(h, hipGetLastError());
+    /* pivots in chunks, the done flag read between them */
+    constexpr int kChunk = 32;
+    const int64_t maxp = sw_lp_max_pivots(&d);
+    for (int64_t done_piv = 0;; done_piv += kChunk) {
+        for (int q = 0; q < kChunk; ++q) {
+            hipLaunchKernelGGL(k_lp_select, dim3(1), dim3(SW_BLOCK), 0, st, num_jobs, num_types, b->tab.p,
+                               b->lbasis.p, b->lf.p, b->lp.p, b->lst.p);
+            hipLaunchKernelGGL(k_lp_update, dim3((unsigned)(d.R + 1)), dim3(kLpTB), 0, st, num_jobs, num_types,
+                               b->tab.p, b->lf.p, b->lp.p, b->lst.p);
+        }
+        MMF_HIP(h, hipGetLastError());
+        MMF_HIP(h, hipMemcpyAsync(b->hlst.p, b->lst.p, sizeof(LpState), hipMemcpyDeviceToHost, st));
+        MMF_HIP(h, hipStreamSynchronize(st));
+        if (b->hlst.p->done != 0 || done_piv > maxp) break;
+    }
+    hipLaunchKernelGGL(k_lp_result, dim3(1), dim3(SW_BLOCK), 0, st, num_jobs, num_types, b->tab.p, b->lbasis.p,
+                       b->lst.p, b->lx.p, b->lout.p);
     MMF_HIP(h, hipGetLastError());
     MMF_HIP(h, hipMemcpyAsync(b->hlx.p, b->lx.p, mn * 8, hipMemcpyDeviceToHost, st));
     MMF_HIP(h, hipMemcpyAsync(b->hlout.p, b->lout.p, 3 * 8, hipMemcpyDeviceToHost, st));
