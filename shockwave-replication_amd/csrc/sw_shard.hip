@@ -1149,11 +1149,51 @@ __global__ __launch_bounds__(kTB) void k_p2x_pre_bits(const int32_t* hdr, const 
 /* the first edge costs of every load size F (each class width): entry
  * (ki, t, u), the cheapest class k with w_k | F, F / w_k ≤ SW_P2X_QMAX
  * (ascending k on ties), without δ — oracle/p2x_twin.c build_w */
+/* sw_p2x_cost (sw_p2x.h) on one wave: lane i holds word i of the and-not
+ * words in scan order (ascending words when u < t, descending when u > t),
+ * 64 words per pass; the q picks are located by a ballot over the lanes'
+ * running popcounts, each pick's rank read back to lane 0, which sums c in
+ * selection order from 0.0 as the sequential form does.  Wave-uniform
+ * result.  (Thread-per-entry, the longest scan — 60 words of a C4 class in
+ * one thread, one L2 round trip per word — set the set-up kernel's 32 µs.) */
+__device__ __forceinline__ double p2x_cost_wave(const uint64_t* Bt, const uint64_t* Bu, int nw, int ws, int q,
+                                                int t, int u, const double* c) {
+    const int lane = lane_id();
+    const bool lo = u < t;
+    double s = 0.0;
+    int got = 0;
+    for (int base = 0; base < nw && got < q; base += 64) {
+        const int i = base + lane;
+        const int w = lo ? i : nw - 1 - i; /* the word this lane holds */
+        const uint64_t x = i < nw ? (Bt[(size_t)w * ws] & ~Bu[(size_t)w * ws]) : 0ull;
+        const int cnt = __popcll(x);
+        const int inc = wave_incscan_i32(cnt);
+        const int tot = __builtin_amdgcn_readlane(inc, 63);
+        const int need = q - got < tot ? q - got : tot;
+        for (int g = 0; g < need; ++g) {
+            /* the lane holding this pass's pick g: the first with inc > g */
+            const int owner = (int)__builtin_ctzll(__ballot(inc > g));
+            int rank = 0;
+            if (lane == owner) {
+                uint64_t y = x;
+                for (int d = g - (inc - cnt); d > 0; --d) /* skip the picks before g in this word */
+                    y = lo ? (y & (y - 1)) : (y & ~(1ull << (63 - __builtin_clzll(y))));
+                rank = 64 * w + (lo ? __builtin_ctzll(y) : 63 - __builtin_clzll(y));
+            }
+            rank = __builtin_amdgcn_readlane(rank, owner);
+            s = s + c[rank];
+        }
+        got += need;
+    }
+    return got == q ? s * (double)(u - t) : SW_P2X_NONE;
+}
+
+/* one wave per entry (ki, t, u) */
 __global__ __launch_bounds__(kTB) void k_p2x_pre_w(const int32_t* hdr, const double* pc,
                                                    const uint64_t* B, int T, double* Wb, int8_t* Wk) {
     const int K = hdr[SW_P2X_HDR_K];
-    const int64_t e = (int64_t)blockIdx.x * kTB + threadIdx.x;
-    if (K <= 0 || e >= (int64_t)K * T * T) return;
+    const int64_t e = ((int64_t)blockIdx.x * kTB + threadIdx.x) >> 6;
+    if (K <= 0 || e >= (int64_t)K * T * T) return; /* uniform over the wave */
     const int ki = (int)(e / (T * T)), tu = (int)(e % (T * T)), t = tu / T, u = tu % T;
     const int F = hdr[SW_P2X_HDR_WC + ki];
     double best = SW_P2X_NONE;
@@ -1163,15 +1203,17 @@ __global__ __launch_bounds__(kTB) void k_p2x_pre_w(const int32_t* hdr, const dou
             const int wk = hdr[SW_P2X_HDR_WC + k];
             if (wk > F || F % wk != 0 || F / wk > SW_P2X_QMAX) continue;
             const uint64_t* Bk = B + (size_t)hdr[SW_P2X_HDR_BOFF + k];
-            const double cost = sw_p2x_cost(Bk + t, Bk + u, hdr[SW_P2X_HDR_NW + k], T, F / wk, t, u,
-                                            pc + hdr[SW_P2X_HDR_OFF + k]);
+            const double cost = p2x_cost_wave(Bk + t, Bk + u, hdr[SW_P2X_HDR_NW + k], T, F / wk, t, u,
+                                              pc + hdr[SW_P2X_HDR_OFF + k]);
             if (cost < best) {
                 best = cost;
                 bk = k;
             }
         }
-    Wb[e] = best;
-    Wk[e] = (int8_t)bk;
+    if (lane_id() == 0) {
+        Wb[e] = best;
+        Wk[e] = (int8_t)bk;
+    }
 }
 
 /* The step on the M gathered entries (entry j = job j), one workgroup, the
@@ -2204,7 +2246,7 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         const int64_t slots = (M + 63) / 64 + SW_P2X_KMAX;
         LAUNCH(S, k_p2x_pre_bits, dim3(nblk(slots * 64)), dim3(kTB), 0, st, hdr, S->porder.p, S->p2ws.p,
                M, T, ord, pc, B);
-        LAUNCH(S, k_p2x_pre_w, dim3(nblk((int64_t)SW_P2X_KMAX * T * T)), dim3(kTB), 0, st, hdr, pc, B, T,
+        LAUNCH(S, k_p2x_pre_w, dim3(nblk((int64_t)SW_P2X_KMAX * T * T * 64)), dim3(kTB), 0, st, hdr, pc, B, T,
                Wb, Wk);
         pre.hdr = hdr;
         pre.ord = ord;
