@@ -176,6 +176,13 @@ def test_gpu_types_rejects_bad_input(gpu_solver):
         gpu_solver.mmf_allocate_types([4, 2], [1, 1], np.array([[1.0, np.nan], [1.0, 1.0]]))
     x, t, p = gpu_solver.mmf_allocate_types([4, 2], [], np.zeros((0, 2)))
     assert x.shape == (0, 2) and t == 0.0
+    # above the limits: too many jobs (invalid), a tableau above 256 MB (capacity)
+    with pytest.raises(sn.NativeError) as e:
+        gpu_solver.mmf_allocate_types([4], np.ones(2049, dtype=np.int32), np.ones((2049, 1)))
+    assert e.value.code == sn.SW_ERR_INVALID
+    with pytest.raises(sn.NativeError) as e:
+        gpu_solver.mmf_allocate_types(np.full(16, 8), np.ones(2048, dtype=np.int32), np.ones((2048, 16)))
+    assert e.value.code == sn.SW_ERR_CAPACITY
 
 
 @pytest.mark.gpu
