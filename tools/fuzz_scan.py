@@ -6,8 +6,9 @@ the twin's, with the fields that differ; batched and single solves.
 
 With --onchip every instance is on-chip (N <= 1024, T <= 32), so the launch
 form follows the chunk size (sw_api.hip launch): <= 256 the full kernel with
-the exchange step fused, 257..1024 the full kernel then sw_p2x_kernel, > 1024
-the split kernels then sw_p2x_kernel.
+the exchange step fused, > 256 the split kernels (level kernel, then the pack
+kernel with the exchange step fused, then the full kernel with it for the
+instances the pack kernel leaves).
 """
 import ctypes
 import os
