@@ -12,7 +12,8 @@
  * r = v, is built once and then kept up to date: a position placed in round t
  * moves w from Hu[r] to Hu[r − 1] (2 LDS atomics per placed position instead
  * of one per position per round — the per-round rebuild was the kernel's LDS
- * bank-conflict hot spot at 10k jobs).  The round's clamped histogram
+ * bank-conflict hot spot at 10k jobs).  Hu is held in SW_HCOPIES copies by
+ * lane (sw_pack_lds::Hc), summed at each round's start.  The round's clamped histogram
  * H[v] = Hu[v] (v < R), H[R] = Σ_{v ≥ R} Hu[v] is formed in registers.  The
  * tier histogram SH is per round and double-buffered by round parity, so
  * each round needs one barrier before its tiers.
@@ -68,7 +69,7 @@ __device__ __forceinline__ uint32_t pk_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t pk_w(uint32_t s) { return (s >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t pk_sel(uint32_t s) { return (s >> 16) & 1u; }
 
-/* LDS the round loop needs: the running histogram Hu (H[0]); the rest is
+/* LDS the round loop needs: the running histogram's copies Hc; H and SH are
  * spare (kept for the carve-up of sw_kernels.hip). */
 #ifndef SW_HCOPIES
 #define SW_HCOPIES 4
@@ -146,26 +147,38 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
     SWP_DECL;
     /* positions past A carry st = 0 (r = 0, w = 0): they fail every
      * eligibility test below, so no per-position bound check is needed */
-    int32_t* Hu = L->H[0];
-    if (tid < 68) Hu[tid] = 0;
+    /* the running histogram in SW_HCOPIES copies by lane (L->Hc, as the
+     * one-wave loop below): the positions a round places mostly share a few
+     * remaining-round counts, and a wave's atomics on one LDS word serialise
+     * over its lanes — with one copy the apply's atomics and the barrier
+     * waiting on them were 48 % of the C4 placement's cycles */
+    int32_t* Hm = L->Hc[lane & (SW_HCOPIES - 1)];
+    for (int x = tid; x < SW_HCOPIES * 72; x += blockDim.x) (&L->Hc[0][0])[x] = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) mk[i] = 0;
     const int32_t cbase = sw_pack_caps_base(caps, T);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < E; ++i)
-        if (st[i] != 0u) atomicAdd(&Hu[pk_r(st[i])], (int32_t)pk_w(st[i]));
+        if (st[i] != 0u) atomicAdd(&Hm[pk_r(st[i])], (int32_t)pk_w(st[i]));
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
         int32_t cap = caps ? caps[t] : G;
         SWP_COUNT(17);
-        __syncthreads(); /* Hu holds the placements of round t − 1 */
+        __syncthreads(); /* the copies hold the placements of round t − 1 */
         /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
          * lane m holds hv = H[m + 1] */
-        const int32_t suf = wave_sufscan_i32(Hu[lane]);
-        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + Hu[64];
-        const int32_t hv = (lane + 1 < R) ? Hu[lane + 1] : (lane + 1 == R ? tailR : 0);
+        int32_t h0 = 0, h1 = 0; /* bins lane and lane + 1, the copies summed */
+#pragma unroll
+        for (int c = 0; c < SW_HCOPIES; ++c) {
+            h0 += L->Hc[c][lane];
+            h1 += L->Hc[c][lane + 1];
+        }
+        const int32_t h64 = __builtin_amdgcn_readlane(h1, 63);
+        const int32_t suf = wave_sufscan_i32(h0);
+        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + h64;
+        const int32_t hv = (lane + 1 < R) ? h1 : (lane + 1 == R ? tailR : 0);
         /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
         const int32_t S0 = wave_sufscan_i32(hv);
         const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
@@ -246,8 +259,8 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             cap -= best & 0xFF;
         }
         SWP_STAMP(4);
-        /* apply (all reads of Hu this round happened before the fill's
-         * barrier): placed positions move their width down one bin */
+        /* apply (all reads of the copies this round happened before the
+         * fill's barrier): placed positions move their width down one bin */
 #pragma unroll
         for (int i = 0; i < E; ++i) {
             const bool sel = pk_sel(st[i]) != 0; /* only existing positions get selected */
@@ -255,8 +268,8 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             mk[i] |= sel ? (1ull << t) : 0ull;
             st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
             if (sel) {
-                atomicAdd(&Hu[r], -(int32_t)pk_w(st[i]));
-                atomicAdd(&Hu[r - 1], (int32_t)pk_w(st[i]));
+                atomicAdd(&Hm[r], -(int32_t)pk_w(st[i]));
+                atomicAdd(&Hm[r - 1], (int32_t)pk_w(st[i]));
             }
         }
         SWP_STAMP(5);

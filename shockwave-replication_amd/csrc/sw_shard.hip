@@ -183,21 +183,30 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
 }
 
 /* key rows (twin: build), A read from the all-reduced step result */
+/* one wave per job, lane n = the job's (n+1)-th round: f(n + 1) − f(n) per
+ * lane, the running minimum over n as a wave prefix-min scan (min is exact,
+ * so any scan order gives the sequential loop's values), the fp32 keys
+ * stored coalesced.  (A thread per job walked its 30 rounds in sequence:
+ * 16 µs per C4 solve, the job loop spread over only NL / 256 workgroups.) */
 __global__ __launch_bounds__(kTB) void k_keys(ShardDev S) {
-    const int i = blockIdx.x * kTB + threadIdx.x;
-    if (i >= S.NL) return;
+    const int64_t i = ((int64_t)blockIdx.x * kTB + threadIdx.x) >> 6;
+    if (i >= S.NL) return; /* uniform over the wave */
+    const int n = lane_id();
     const double A = sw_from_bits((uint64_t)S.red[0]);
     const sw_jobc c = S.jc[i];
     const double ks = sw_key_scale(c.w, A);
-    float* row = S.keys + (size_t)i * S.T;
-    double prev = sw_f(&c, 0, S.nb, S.beta, S.ell, S.slope), vm = 0.0;
-    for (int n = 0; n < S.T; ++n) {
+    double v = 0.0;
+    if (n < S.T) {
+        const double prev = sw_f(&c, n, S.nb, S.beta, S.ell, S.slope);
         const double cur = sw_f(&c, n + 1, S.nb, S.beta, S.ell, S.slope);
-        const double v = sw_pos(cur - prev);
-        vm = (n == 0) ? v : sw_min(vm, v);
-        row[n] = sw_key(vm, ks);
-        prev = cur;
+        v = sw_pos(cur - prev);
     }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(v, o, 64);
+        if (n >= o) v = sw_min(u, v);
+    }
+    if (n < S.T) S.keys[(size_t)i * S.T + n] = sw_key(v, ks);
 }
 
 /* ---- SELECT steps ----------------------------------------------------------- */
@@ -712,18 +721,26 @@ struct alignas(16) key2 {
 };
 
 /* Global placement order of the gathered entries, by sorting: each
- * kSortChunk-entry chunk is bitonic-sorted in LDS (descending; inactive
- * entries as (0, 0), which every active key exceeds, sort last), then each
- * active entry's global rank is its chunk position plus, for every other
- * chunk, the number of its keys above the entry's key (a binary search in
- * that sorted chunk).  Keys are unique, so the ranks of the active entries
- * are a permutation of [0, A); order[rank] = entry. */
-constexpr int kSortChunk = 1024;
-constexpr int kSortThreads = kSortChunk / 2;
+ * kSortChunk-entry chunk is bitonic-sorted (descending; inactive entries as
+ * (0, 0), which every active key exceeds, sort last), then each active
+ * entry's global rank is its chunk position plus, for every other chunk, the
+ * number of its keys above the entry's key (a binary search in that sorted
+ * chunk).  Keys are unique, so the ranks of the active entries are a
+ * permutation of [0, A); order[rank] = entry. */
+constexpr int kSortChunk = 256;
+constexpr int kSortThreads = kSortChunk; /* one entry per thread */
 __device__ __forceinline__ bool key_gt(const key2& a, const key2& b) {
     return a.h > b.h || (a.h == b.h && a.l > b.l);
 }
-/* nact (optional): the entries are compacted, the first *nact active —
+/* One entry per thread, in registers.  Stage (kk, jj) pairs position p with
+ * p ^ jj: partners within a wave (jj < 64) trade through cross-lane shuffles,
+ * with no barrier; the 10 stages with jj ≥ 64 through LDS.  Both partners
+ * evaluate the same exchange test on the same pair (a = the lower position's
+ * entry), so they agree on it, and the network and its exchanges are the
+ * LDS-only form's: the same sorted chunk.  (The LDS-only form, 512 threads
+ * with one pair each and a barrier per stage, took 19–20 µs per 10k-entry
+ * sort)
+ * nact (optional): the entries are compacted, the first *nact active —
  * chunks past them have nothing to sort */
 __global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_ent* all, int64_t M,
                                                                    key2* skeys, int32_t* sidx,
@@ -733,56 +750,77 @@ __global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_
     const int64_t c0 = (int64_t)blockIdx.x * kSortChunk;
     const int64_t na = nact ? (int64_t)*nact : M;
     if (c0 >= na) return;
-    for (int x = threadIdx.x; x < kSortChunk; x += kSortThreads) {
-        const int64_t e = c0 + x;
-        key2 v;
-        v.h = 0; v.l = 0;
-        if (e < M && e < na && all[e].st != 0) { v.h = all[e].khi; v.l = all[e].klo; }
-        k[x] = v;
-        ix[x] = (int32_t)e;
-    }
-    __syncthreads();
-    const int t = threadIdx.x; /* one compare-exchange pair per thread and stage */
+    const int p = threadIdx.x;
+    key2 v;
+    v.h = 0; v.l = 0;
+    const int64_t e = c0 + p;
+    if (e < M && e < na && all[e].st != 0) { v.h = all[e].khi; v.l = all[e].klo; }
+    int32_t vi = (int32_t)e;
     for (int kk = 2; kk <= kSortChunk; kk <<= 1) {
         for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            const int i = 2 * t - (t & (jj - 1)); /* bit jj of i is clear */
-            const int q = i + jj;
-            const bool desc = (i & kk) == 0;
-            const key2 a = k[i], b = k[q];
-            if (desc ? key_gt(b, a) : key_gt(a, b)) {
-                k[i] = b; k[q] = a;
-                const int32_t ti = ix[i]; ix[i] = ix[q]; ix[q] = ti;
+            key2 o;
+            int32_t oi;
+            if (jj >= 64) {
+                k[p] = v;
+                ix[p] = vi;
+                __syncthreads();
+                o = k[p ^ jj];
+                oi = ix[p ^ jj];
+                __syncthreads();
+            } else {
+                o.h = __shfl_xor(v.h, jj, 64);
+                o.l = __shfl_xor(v.l, jj, 64);
+                oi = __shfl_xor(vi, jj, 64);
             }
-            __syncthreads();
+            const bool lower = (p & jj) == 0;
+            const bool desc = (p & kk) == 0;
+            const key2& a = lower ? v : o;
+            const key2& b = lower ? o : v;
+            if (desc ? key_gt(b, a) : key_gt(a, b)) { v = o; vi = oi; }
         }
     }
-    for (int x = threadIdx.x; x < kSortChunk; x += kSortThreads) {
-        skeys[c0 + x] = k[x];
-        sidx[c0 + x] = ix[x];
-    }
+    skeys[c0 + p] = v;
+    sidx[c0 + p] = vi;
 }
 
+/* One thread per (entry, chunk): lane q of an entry's group of kMergeG
+ * searches chunk q (11 halving steps for the number of its keys above the
+ * entry's key: the descending chunk's prefix where ck[i] > v), and the group
+ * sums its counts with shuffles.  One thread per entry searching every chunk
+ * in turn put ~110 scattered L2 loads per thread on the 40 CUs its 10k
+ * threads fill (15 µs per C4 sort; 23 µs with the searches interleaved); the
+ * (entry, chunk) grid spreads them over the chip. */
+constexpr int kMergeG = 64; /* lanes per entry, a wave (more chunks: lane q searches q, q + 64, …) */
 __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, const int32_t* sidx,
                                                          int nchunks, int32_t* order,
                                                          const int32_t* nact = nullptr) {
-    const int64_t s = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * kTB + threadIdx.x;
     if (nact) nchunks = (int)((*nact + kSortChunk - 1) / kSortChunk);
-    if (s >= (int64_t)nchunks * kSortChunk) return;
-    const key2 v = skeys[s];
-    if (v.h == 0 && v.l == 0) return; /* inactive or padding */
+    const int64_t s = g / kMergeG; /* groups of kMergeG lanes lie inside one wave */
+    const int q = (int)(g % kMergeG);
+    const bool live = s < (int64_t)nchunks * kSortChunk;
+    key2 v;
+    v.h = 0; v.l = 0;
+    if (live) v = skeys[s];
     const int c = (int)(s / kSortChunk);
-    int64_t r = s - (int64_t)c * kSortChunk;
-    for (int c2 = 0; c2 < nchunks; ++c2) {
-        if (c2 == c) continue;
-        const key2* ck = skeys + (int64_t)c2 * kSortChunk;
-        int lo = 0, hi = kSortChunk; /* first position whose key is not above v */
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (key_gt(ck[mid], v)) lo = mid + 1; else hi = mid;
+    int64_t cnt = 0;
+    if (live && (v.h | v.l) != 0)
+        for (int qq = q; qq < nchunks; qq += kMergeG) { /* chunks q, q + kMergeG, … */
+            if (qq == c) continue;
+            const key2* ck = skeys + (int64_t)qq * kSortChunk;
+            int pos = 0;
+#pragma unroll
+            for (int step = kSortChunk; step > 0; step >>= 1) {
+                const int i = pos + step - 1;
+                if (i < kSortChunk && key_gt(ck[i], v)) pos += step;
+            }
+            cnt += pos;
         }
-        r += lo;
-    }
-    order[r] = sidx[s];
+    int pos = (int)cnt;
+#pragma unroll
+    for (int o = kMergeG / 2; o > 0; o >>= 1) pos += __shfl_xor(pos, o, 64);
+    if (!live || q != 0 || (v.h == 0 && v.l == 0)) return; /* inactive or padding */
+    order[s - (int64_t)c * kSortChunk + pos] = sidx[s];
 }
 
 /* the round loop over the global order; writes this rank's rows */
@@ -933,10 +971,13 @@ int wave_pack_max() {
 
 /* The round loop for up to 8·NT active entries with E = 2, 4 or 8 positions
  * per thread chosen by A at run time (one launch; the E = 8 body sets the
- * registers, well inside the budget): the per-position loops of every pass
+ * registers, well inside the budget) — and with EB = 20 up to 20·NT in the
+ * same launch (one workgroup per placement, so the wider body's registers
+ * cost no occupancy; a second kernel that only counted A and returned was
+ * 5 µs per C4 placement): the per-position loops of every pass
  * walk what the entries need, not what M allows — a rank's share placement
  * has M = its job count but A = its jobs with rounds (≈ 3/8 of them at C4). */
-template <int NT>
+template <int NT, int EB>
 __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pack_ent* all, int64_t M,
                                                         const int32_t* order, uint64_t* ydst, int32_t* pdst,
                                                         CapsArg caps, int alo, int zero) {
@@ -951,12 +992,15 @@ __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pac
     int act = 0;
     for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
-    if (A <= alo || A > 8 * NT) return; /* another variant places these */
+    if (A <= alo || A > (EB > 8 ? EB : 8) * NT) return; /* another variant places these */
     if (zero) /* a whole placement (not one width class): every row of this rank */
         for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
     if (A <= 2 * NT) pack_rounds_body<2>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
     else if (A <= 4 * NT) pack_rounds_body<4>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
-    else pack_rounds_body<8>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    else if (EB <= 8 || A <= 8 * NT)
+        pack_rounds_body<8>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    else
+        pack_rounds_body<(EB > 8 ? EB : 8)>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
 }
 
 /* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
@@ -1818,7 +1862,7 @@ int op_setup(void* ctx, double* A, double* lb, double* top) {
         SH_HIP(S, hipMemcpyAsync(S->dv.red, S->hx.p, 16, hipMemcpyHostToDevice, st));
         SH_HIP(S, hipStreamSynchronize(st));
     }
-    LAUNCH(S, k_keys, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv);
+    LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv);
     *A = sw_from_bits(mx[0]);
     *lb = sw_from_bits(mx[1]);
     *top = sw_from_bits(mx[3]);
@@ -2070,7 +2114,7 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
     LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, all, M, S->skeys.p,
            S->sidx.p);
-    LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
+    LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk * kMergeG)), dim3(kTB), 0, st, S->skeys.p,
            S->sidx.p, nch, S->porder.p);
     const ShardDev dv = S->dv;
     uint64_t* yd = S->y[ydst].p;
@@ -2089,8 +2133,8 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
         LAUNCH(S, k_pack_rounds_wave, dim3(1), dim3(64), 0, st, dv, all, M, S->porder.p, yd, pd, capsd, wa,
                (int)(mode != 5));
     const int lo = wave ? wa : -1;
-#define SW_LAUNCH_SEL(NT, ALO)                                                                  \
-    LAUNCH(S, (k_pack_rounds_sel<NT>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, pd, \
+#define SW_LAUNCH_SEL(NT, EB, ALO)                                                                  \
+    LAUNCH(S, (k_pack_rounds_sel<NT, EB>), dim3(1), dim3(NT), 0, st, dv, all, M, S->porder.p, yd, pd, \
            capsd, (int)(ALO), (int)(mode != 5))
     /* measured on C4's share placement (profiles/r7nt1_*): E by the active
      * entries in one launch against E by the entries, rank loop 148 → 125 µs
@@ -2099,10 +2143,15 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     if (wave && M <= wa) {
     } else if (M <= 64 * SW_BLOCK) {
         /* E by the active entries: one launch up to 8·512 of them */
-        SW_LAUNCH_SEL(SW_BLOCK, lo);
-        if (M > 32 * SW_BLOCK) SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
-        else if (M > 20 * SW_BLOCK) SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
-        else if (M > 8 * SW_BLOCK) SW_LAUNCH_PACK(20, SW_BLOCK, 8 * SW_BLOCK);
+        if (M <= 8 * SW_BLOCK) {
+            SW_LAUNCH_SEL(SW_BLOCK, 0, lo);
+        } else if (M <= 20 * SW_BLOCK) {
+            SW_LAUNCH_SEL(SW_BLOCK, 20, lo);
+        } else {
+            SW_LAUNCH_SEL(SW_BLOCK, 0, lo);
+            if (M > 32 * SW_BLOCK) SW_LAUNCH_PACK(64, SW_BLOCK, 8 * SW_BLOCK);
+            else SW_LAUNCH_PACK(32, SW_BLOCK, 8 * SW_BLOCK);
+        }
     } else {
         return S->h->err = "sharded placement holds at most 32768 jobs", SW_ERR_CAPACITY;
     }
@@ -2241,7 +2290,7 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
         LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, S->p2keys.p, M, S->skeys.p,
                S->sidx.p, (const int32_t*)(hdr + SW_P2X_HDR_A));
-        LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk)), dim3(kTB), 0, st, S->skeys.p,
+        LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk * kMergeG)), dim3(kTB), 0, st, S->skeys.p,
                S->sidx.p, nch, S->porder.p, (const int32_t*)(hdr + SW_P2X_HDR_A));
         const int64_t slots = (M + 63) / 64 + SW_P2X_KMAX;
         LAUNCH(S, k_p2x_pre_bits, dim3(nblk(slots * 64)), dim3(kTB), 0, st, hdr, S->porder.p, S->p2ws.p,
@@ -2416,11 +2465,12 @@ extern "C" {
 
 #ifdef SW_STAMPS
 /* Diagnostic builds only (not part of include/shockwave_amd.h): round-loop
- * phase cycles accumulated since the last call (which also clears them). */
+ * phase cycles and counters (24 words, sw_pack.h SWP_FLUSH) accumulated since
+ * the last call (which also clears them). */
 int sw_debug_pack_stamps(uint64_t* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sw_pack_stamps), 8 * sizeof(uint64_t)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sw_pack_stamps), 24 * sizeof(uint64_t)) != hipSuccess)
         return SW_ERR_HIP;
-    uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t z[24] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_sw_pack_stamps), z, sizeof(z)) == hipSuccess ? SW_OK : SW_ERR_HIP;
 }
 #endif

@@ -4,7 +4,8 @@
 
 Solves one C4 instance on the sharded engine at world 1 with the stamps
 library and prints the cycles per phase of k_pack_rounds (thread 0's
-s_memtime view; shader-clock cycles, summed over the solve's packs)."""
+s_memtime view; shader-clock cycles, summed over the solve's packs) and the
+loop's counters: rounds, active tiers, width-tail reductions."""
 import ctypes as C
 import os
 import sys
@@ -25,7 +26,7 @@ def main():
         s = sn.Solver(device=0, lib=lib)
         s.dist_init(sn.unique_id(lib), 0, 1)
         s.dist_solve(a, 0, a.N)
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 24)()
         lib.sw_debug_pack_stamps(out)
         s.dist_solve(a, 0, a.N)
         lib.sw_debug_pack_stamps(out)
@@ -33,6 +34,7 @@ def main():
         print(f"N={N}: round-loop cycles per solve {tot}")
         for i, n in enumerate(NAMES):
             print(f"   {n:10s} {out[i]:10d} {100.0 * out[i] / max(tot, 1):5.1f}%")
+        print(f"   rounds {out[17]}  tiers {out[18]}  tail reductions {out[19]}")
         s.close()
 
 
