@@ -134,6 +134,39 @@ __device__ __forceinline__ int32_t sw_pack_room(const int32_t* caps, int t, int 
     return x > 0 ? pv : 0;
 }
 
+/* The histogram copies → the cumulative form C[v] = Σ_{u ≥ v} Hu[u] in copy
+ * 0 (the other copies zeroed), by one wave (its LDS reads issue before its
+ * writes).  In that form a position placed in round t (r → r − 1) changes
+ * C[r] alone — one atomic instead of two — and the round's need is one
+ * suffix sum (sw_pack_need). */
+__device__ __forceinline__ void sw_pack_cum(sw_pack_lds* L) {
+    const int lane = lane_id();
+    int32_t h = 0, h64 = 0;
+#pragma unroll
+    for (int c = 0; c < SW_HCOPIES; ++c) {
+        h += L->Hc[c][lane];
+        h64 += L->Hc[c][64];
+    }
+    const int32_t C = wave_sufscan_i32(h) + h64;
+#pragma unroll
+    for (int c = 0; c < SW_HCOPIES; ++c) {
+        L->Hc[c][lane] = c == 0 ? C : 0;
+        if (lane < 8) L->Hc[c][64 + lane] = (c == 0 && lane == 0) ? h64 : 0;
+    }
+}
+
+/* need_m = Σ_{v>m} (v−m)·H[v] − room_m over the round's clamped histogram
+ * (H[v] = Hu[v] for v < R, H[R] = Σ_{v ≥ R} Hu[v]), lane m < R (−1 above):
+ * by parts, Σ_{v>m} (v−m)·H[v] = Σ_{v=m+1}^{R} C[v] — the same integer. */
+__device__ __forceinline__ int32_t sw_pack_need(const sw_pack_lds* L, int R, int32_t room) {
+    const int lane = lane_id();
+    int32_t c1 = 0; /* C[lane + 1], the copies summed */
+#pragma unroll
+    for (int c = 0; c < SW_HCOPIES; ++c) c1 += L->Hc[c][lane + 1];
+    const int32_t D = wave_sufscan_i32(lane + 1 <= R ? c1 : 0);
+    return lane < R ? D - room : -1;
+}
+
 /* caps: per-round capacity in LDS (nullptr = G every round) — the class-wise
  * P2 repack, where positions carry unit widths */
 template <int E, class BLK>
@@ -161,29 +194,16 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
 #pragma unroll
     for (int i = 0; i < E; ++i)
         if (st[i] != 0u) atomicAdd(&Hm[pk_r(st[i])], (int32_t)pk_w(st[i]));
+    __syncthreads();
+    if (tid < 64) sw_pack_cum(L); /* the first round's barrier publishes it */
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
         int32_t cap = caps ? caps[t] : G;
         SWP_COUNT(17);
         __syncthreads(); /* the copies hold the placements of round t − 1 */
-        /* clamped histogram H[v] = Hu[v] (v < R), H[R] = Σ_{v≥R} Hu[v];
-         * lane m holds hv = H[m + 1] */
-        int32_t h0 = 0, h1 = 0; /* bins lane and lane + 1, the copies summed */
-#pragma unroll
-        for (int c = 0; c < SW_HCOPIES; ++c) {
-            h0 += L->Hc[c][lane];
-            h1 += L->Hc[c][lane + 1];
-        }
-        const int32_t h64 = __builtin_amdgcn_readlane(h1, 63);
-        const int32_t suf = wave_sufscan_i32(h0);
-        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + h64;
-        const int32_t hv = (lane + 1 < R) ? h1 : (lane + 1 == R ? tailR : 0);
-        /* need_m = Σ_{v>m} (v−m)·H[v] − G·(R−1−m), lane m (every wave alike) */
-        const int32_t S0 = wave_sufscan_i32(hv);
-        const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-        const int32_t room = sw_pack_room(caps, t, R, G, cbase);
-        const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
+        /* need_m, lane m (every wave alike) */
+        const int32_t need = sw_pack_need(L, R, sw_pack_room(caps, t, R, G, cbase));
         SWP_STAMP(1);
         /* tiers: jobs with more than m rounds left must shed enough now */
         int mstart = R - 1;
@@ -267,10 +287,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             const uint32_t r = pk_r(st[i]);
             mk[i] |= sel ? (1ull << t) : 0ull;
             st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
-            if (sel) {
-                atomicAdd(&Hm[r], -(int32_t)pk_w(st[i]));
-                atomicAdd(&Hm[r - 1], (int32_t)pk_w(st[i]));
-            }
+            if (sel) atomicAdd(&Hm[r], -(int32_t)pk_w(st[i])); /* C[r] alone */
         }
         SWP_STAMP(5);
     }
@@ -323,6 +340,8 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
 #pragma unroll
     for (int i = 0; i < E1; ++i)
         if (st[i] != 0u) atomicAdd(&Hm[RR_(i)], WW_(i));
+    wave_sync();
+    sw_pack_cum(L);
     const int32_t cbase = sw_pack_caps_base(caps, T);
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
@@ -331,20 +350,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
         SWP_COUNT(17);
         SWP_STAMP(9); /* diagnostic: the cost of one stamp */
         wave_sync(); /* the copies hold the placements of round t − 1 */
-        int32_t h0 = 0, h1 = 0; /* bins lane and lane + 1, the copies summed */
-#pragma unroll
-        for (int c = 0; c < SW_HCOPIES; ++c) {
-            h0 += L->Hc[c][lane];
-            h1 += L->Hc[c][lane + 1];
-        }
-        const int32_t h64 = __builtin_amdgcn_readlane(h1, 63);
-        const int32_t suf = wave_sufscan_i32(h0);
-        const int32_t tailR = (R < 64 ? __builtin_amdgcn_readlane(suf, R) : 0) + h64;
-        const int32_t hv = (lane + 1 < R) ? h1 : (lane + 1 == R ? tailR : 0);
-        const int32_t S0 = wave_sufscan_i32(hv);
-        const int32_t S1 = wave_sufscan_i32(hv * (lane + 1));
-        const int32_t room = sw_pack_room(caps, t, R, G, cbase);
-        const int32_t need = (lane < R) ? (S1 - lane * S0) - room : -1;
+        const int32_t need = sw_pack_need(L, R, sw_pack_room(caps, t, R, G, cbase));
         SWP_STAMP(1);
         int mstart = R - 1;
         int32_t red = 0;
@@ -421,8 +427,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
             const int32_t r = RR_(i);
             const bool sel = RA_(i) == 0 && r > 0;
             if (sel) {
-                atomicAdd(&Hm[r], -WW_(i));
-                atomicAdd(&Hm[r - 1], WW_(i));
+                atomicAdd(&Hm[r], -WW_(i)); /* C[r] alone */
                 atomicOr((unsigned long long*)&xmk[E1 * lane + i], 1ull << t);
             }
             const uint32_t r2 = (uint32_t)(r - (sel ? 1 : 0));

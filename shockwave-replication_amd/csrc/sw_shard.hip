@@ -108,6 +108,17 @@ struct ShardDev {
     uint8_t* plan;
     int32_t* planned;
     long long* red; /* i64 / u64-bit step results */
+    /* fused publish (world 1): the kernel's last block stores the step result
+     * into pinned host memory and releases the flag itself, instead of a
+     * k_publish launch behind it (dst = nullptr: not armed) */
+    struct {
+        uint32_t* dst;
+        unsigned long long* flag;
+        unsigned long long seq;
+        const uint32_t* src;
+        const int* xerr;
+        int nwords;
+    } pub;
 };
 
 struct Thresholds {
@@ -154,6 +165,37 @@ __device__ __forceinline__ void red_umax(long long* dst, uint64_t v) {
     if (lane_id() == 0 && v != 0) atomicMax((unsigned long long*)dst, (unsigned long long)v);
 }
 
+/* The step result to the host (k_publish's stores, by one whole block): the
+ * words read at device scope (other blocks' atomics and stores), then the
+ * error word, a system-scope fence and the flag's release.  Plain vector
+ * stores, no scalar-cache writes. */
+__device__ __forceinline__ void pub_store(const ShardDev& S) {
+    for (int i = threadIdx.x; i < S.pub.nwords; i += blockDim.x)
+        S.pub.dst[i] = __hip_atomic_load(S.pub.src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) S.pub.dst[S.pub.nwords] = S.pub.xerr ? (uint32_t)*S.pub.xerr : 0u;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(S.pub.flag, S.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr int kRedCtr = 120; /* a step-result slot no step uses: the last-block counter */
+/* At the end of a step kernel, by every thread that did not return: when
+ * armed, the last block to finish (counter red[kRedCtr], zero in every fresh
+ * step slice) publishes.  Uniform over the grid: S.pub is a kernel argument. */
+__device__ __forceinline__ void pub_tail(const ShardDev& S) {
+    if (!S.pub.dst) return;
+    __shared__ int last_;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last_ = atomicAdd((unsigned long long*)(S.red + kRedCtr), 1ull) == (unsigned long long)(gridDim.x - 1);
+    __syncthreads();
+    if (!last_) return;
+    __threadfence();
+    pub_store(S);
+}
+
 /* ---- setup ---------------------------------------------------------------- */
 
 __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const int32_t* w,
@@ -180,6 +222,7 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
     red_umax(S.red + 1, lb);
     red_umax(S.red + 2, bad);
     red_umax(S.red + 3, top);
+    pub_tail(S);
 }
 
 /* key rows (twin: build), A read from the all-reduced step result */
@@ -224,6 +267,7 @@ __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf)
     }
     red_add(S.red + 0, wf);
     red_add(S.red + 1, wall);
+    pub_tail(S);
 }
 
 /* K probes at once: item (job, n) adds w to bin #{m : thr_m < v(n)} (v =
@@ -382,11 +426,17 @@ __global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned lo
 }
 
 /* the last round's step, in place (one wave) */
-__global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, const long long* bins) {
+__global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, const long long* bins,
+                                                     ShardDev S) {
     __shared__ unsigned long long xs[4];
     search_step_wave(sr, bins, xs);
     __syncthreads();
     if (threadIdx.x < 4) sr[threadIdx.x] = xs[threadIdx.x];
+    if (S.pub.dst) { /* one wave: the state to the host (fused publish) */
+        __threadfence();
+        __syncthreads();
+        pub_store(S);
+    }
 }
 
 __global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b) {
@@ -399,6 +449,7 @@ __global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b)
         cnt = d > 0 ? d : 0;
     }
     red_add(S.red + 0, cnt);
+    pub_tail(S);
 }
 
 __global__ __launch_bounds__(kTB) void k_take_all(ShardDev S) {
@@ -434,6 +485,7 @@ __global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
         for (int w = 0; w < kTB / 64; ++w) s += ws[w];
         S.tieblk[blockIdx.x] = s;
     }
+    pub_tail(S);
 }
 
 /* tie group in job order (twin: the excl loop of select_level): thread per
@@ -475,6 +527,7 @@ __global__ __launch_bounds__(kTB) void k_assign(ShardDev S, long long rem, long 
         used = wj * tt;
     }
     red_add(S.red + 0, used);
+    pub_tail(S);
 }
 
 __global__ __launch_bounds__(kTB) void k_tail_best(ShardDev S, long long rem2) {
@@ -533,7 +586,6 @@ __global__ void k_fill_apply(ShardDev S, int i, int t) {
  * block to finish (counter red[kRedCtr]) copies them behind the lanes.
  * out = [A lanes][B lanes][gm][isum].  SW_EV_FINAL also writes the plan row
  * and count of each job. */
-constexpr int kRedCtr = 120; /* a step-result slot no step uses: eval's block counter */
 __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t* arr,
                                              const uint64_t* ysrc, int arr_a, int arr_b, int lpb,
                                              double* out) {
@@ -624,6 +676,11 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
         out[2 * S.LW] = sw_from_bits(g);
         reinterpret_cast<long long*>(out)[2 * S.LW + 1] = (long long)t;
     }
+    if (last && S.pub.dst) { /* the lanes and the two results to the host */
+        __threadfence();
+        __syncthreads();
+        pub_store(S);
+    }
 }
 
 /* ---- placement ---------------------------------------------------------------- */
@@ -695,6 +752,7 @@ __global__ __launch_bounds__(kTB) void k_load(ShardDev S, const int32_t* src) {
     long long v = 0;
     if (i < S.NL) v = (long long)S.jc[i].w * src[i];
     red_add(S.red, v);
+    pub_tail(S);
 }
 
 __global__ __launch_bounds__(kTB) void k_copy_words(uint32_t* dst, const uint32_t* src, int64_t n) {
@@ -1306,6 +1364,11 @@ __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all
             if (j >= S.off && j < S.off + S.NL) ydst[j - S.off] = X.cm[i];
         }
     if (threadIdx.x == 0) S.red[0] = nc;
+    if (S.pub.dst) { /* one workgroup: it is the last */
+        __threadfence();
+        __syncthreads();
+        pub_store(S);
+    }
 }
 
 /* ---- per-round re-optimisation (sw_reround_dev.h) on the gathered P1 plan ----
@@ -1588,6 +1651,12 @@ struct sw_shard_state {
     unsigned long long* pub_flag = nullptr;
     unsigned long long* pub_flag_dev = nullptr;
     unsigned long long pub_seq = 0;
+    /* a step kernel armed to publish its own result (arm_pub): the sequence
+     * number it releases and the device words it stores, consumed by the
+     * publish() of the same words */
+    unsigned long long armed_seq = 0;
+    const void* armed_src = nullptr;
+    size_t armed_bytes = 0;
     int32_t rank = 0, world = 1;
     ncclComm_t comm = nullptr;
     bool host_comm = false;
@@ -1724,6 +1793,12 @@ int publish_wait(sw_shard_state* S, unsigned long long seq, size_t words, size_t
 int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
     const size_t words = (bytes + 3) / 4;
     if (bytes % 4 != 0) return S->h->err = "publish: size not a multiple of 4", SW_ERR_INVALID;
+    if (S->armed_seq) { /* the step kernel publishes these words itself */
+        const unsigned long long seq = S->armed_seq;
+        S->armed_seq = 0;
+        if (S->armed_src == dsrc && S->armed_bytes == bytes) return publish_wait(S, seq, words, bytes, hout);
+        /* not these words: its release precedes the one below, which is waited for */
+    }
     SH_TRY(publish_reserve(S, words));
     const unsigned long long seq = ++S->pub_seq;
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, S->h->stream, (const uint32_t*)dsrc,
@@ -1731,6 +1806,30 @@ int publish(sw_shard_state* S, const void* dsrc, size_t bytes, void* hout) {
     SH_HIP(S, hipGetLastError());
     return publish_wait(S, seq, words, bytes, hout);
 }
+
+/* Fused publish (world 1, no peer transport, no host collectives): the step
+ * kernel launched next stores `bytes` of `dsrc` into the pinned buffer and
+ * releases the flag from its last block (pub_tail / pub_store), so the
+ * host's publish() of the same words only waits — no k_publish launch, whose
+ * dispatch sat between the step kernel and the host on every
+ * host-synchronised step (13 per C4 solve).  disarm_pub after the launch. */
+int arm_pub(sw_shard_state* S, const void* dsrc, size_t bytes) {
+    S->dv.pub.dst = nullptr;
+    if (S->world != 1 || S->peer || S->host_comm || bytes % 4 != 0) return SW_OK;
+    const size_t words = bytes / 4;
+    SH_TRY(publish_reserve(S, words));
+    S->armed_seq = ++S->pub_seq;
+    S->armed_src = dsrc;
+    S->armed_bytes = bytes;
+    S->dv.pub.dst = S->pub_dev;
+    S->dv.pub.flag = S->pub_flag_dev;
+    S->dv.pub.seq = S->armed_seq;
+    S->dv.pub.src = (const uint32_t*)dsrc;
+    S->dv.pub.xerr = (const int*)S->xerr;
+    S->dv.pub.nwords = (int)words;
+    return SW_OK;
+}
+inline void disarm_pub(sw_shard_state* S) { S->dv.pub.dst = nullptr; }
 
 /* One peer-transport collective (k_xchg) on the handle's stream. */
 /* hout (optional): the result also comes to the host (fused publish) */
@@ -1831,6 +1930,7 @@ int coll_gather(sw_shard_state* S, const void* dsend, void* drecv, size_t bytes,
  * the whole ring is cleared once per kRing steps instead of a memset per step. */
 int zero_red(sw_shard_state* S, int n) {
     (void)n;
+    S->dv.pub.dst = nullptr; /* a step's kernels publish only when armed for it */
     if (S->ring_pos >= kRing) {
         SH_HIP(S, hipMemsetAsync(S->red.p, 0, (size_t)kRing * kRed * 8, S->h->stream));
         S->ring_pos = 0;
@@ -1852,8 +1952,10 @@ int op_setup(void* ctx, double* A, double* lb, double* top) {
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
     SH_TRY(zero_red(S, 4));
+    SH_TRY(arm_pub(S, S->dv.red, 32));
     LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->in_w, S->in_d, S->in_F,
            S->in_E, S->in_R, S->delta);
+    disarm_pub(S);
     uint64_t mx[4];
     SH_TRY(coll_reduce(S, S->dv.red, 4, 1, mx));
     if (mx[2]) return S->h->err = "invalid problem (per-job inputs)", SW_ERR_INVALID; /* every rank */
@@ -1888,7 +1990,9 @@ int op_widths(void* ctx, int32_t* w_all) {
 int op_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 2));
+    SH_TRY(arm_pub(S, S->dv.red, 16));
     LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, M, (int)is_inf);
+    disarm_pub(S);
     return coll_reduce(S, S->dv.red, 2, 0, out);
 }
 
@@ -1965,7 +2069,9 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
         prev = S->dv.red;
     }
     unsigned long long* sr = sb + 4 * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
-    LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev);
+    SH_TRY(arm_pub(S, sr, 32));
+    LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev, S->dv);
+    disarm_pub(S);
     unsigned long long v[4];
     SH_TRY(publish(S, sr, sizeof(v), v));
     *out = v[0];
@@ -1976,7 +2082,9 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
 int op_between(void* ctx, double a, double b, int64_t* out) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
+    SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_between, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, a, b);
+    disarm_pub(S);
     return coll_reduce(S, S->dv.red, 1, 0, out);
 }
 
@@ -1989,7 +2097,9 @@ int op_take_all(void* ctx) {
 int op_take(void* ctx, uint32_t rho, int64_t* wt, int64_t* excl) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 2));
+    SH_TRY(arm_pub(S, S->dv.red, 16));
     LAUNCH(S, k_take, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, rho);
+    disarm_pub(S);
     std::vector<int64_t> all((size_t)2 * S->world);
     SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 16, all.data()));
     *wt = 0;
@@ -2005,8 +2115,10 @@ int op_assign(void* ctx, uint32_t rho, int64_t rem, int64_t excl, int64_t* used)
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
     (void)rho; /* k_take stored the tie counts at rho */
+    SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_assign, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, (long long)rem,
            (long long)excl);
+    disarm_pub(S);
     return coll_reduce(S, S->dv.red, 1, 0, used);
 }
 
@@ -2051,8 +2163,10 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     const int lpb = (int)std::max<int64_t>(1, kTB / S->q);
     double* xs = S->xrecv.p + (size_t)S->rank * blk; /* in-place all-gather */
     if (S->q > kTB) return S->h->err = "eval: more than 256 jobs per lane", SW_ERR_CAPACITY;
+    SH_TRY(arm_pub(S, xs, (size_t)blk * 8));
     LAUNCH(S, k_eval, dim3((unsigned)((LW + lpb - 1) / lpb)), dim3(kTB), 0, S->h->stream, S->dv,
            (int)sel, arr, ys, (int)(arg & 0xFF), (int)(arg >> 8), lpb, xs);
+    disarm_pub(S);
     std::vector<double> all((size_t)blk * S->world);
     SH_TRY(coll_gather(S, xs, S->xrecv.p, (size_t)blk * 8, all.data()));
     double g = 0.0;
@@ -2169,7 +2283,9 @@ int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32
 int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
+    SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_load, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p);
+    disarm_pub(S);
     std::vector<int64_t> loads((size_t)S->world);
     SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 8, loads.data()));
     S->share = sw_share_caps(loads.data(), S->world, S->rank, S->T, S->dv.G, S->scaps) == 0;
@@ -2304,8 +2420,10 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         pre.Wb = Wb;
         pre.Wk = Wk;
     }
+    SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_p2x, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, (const p2x_ent*)gv, M, S->p2ws.p,
            S->y[ysrc].p, pre, (int)prepared);
+    disarm_pub(S);
     uint64_t nc = 0;
     SH_TRY(coll_reduce(S, S->dv.red, 1, 1, &nc)); /* every rank computed the same count */
     *cancels = (int32_t)nc;
