@@ -111,7 +111,7 @@ def parse():
     ap.add_argument("--transport", choices=("rccl", "peer"), default="rccl",
                     help="--workload c4: step collectives on RCCL, or on the peer-memory transport "
                          "(sw_dist_enable_peer; at one rank RCCL stays)")
-    ap.add_argument("--c4-steps", dest="c4_steps", type=int, default=20,
+    ap.add_argument("--c4-steps", dest="c4_steps", type=int, default=100,
                     help="sharded C4 solves timed for the c4_sharded sub-record")
     ap.add_argument("--no-c4", dest="no_c4", action="store_true",
                     help="skip the sharded C4 sub-record of the default line")
