@@ -149,6 +149,13 @@ def test_gpu_shard_device_rejects_bad_input(rccl_solver):
     torch.cuda.synchronize()
     r = rccl_solver.dist_solve_dev(shard, 0, a.N)  # the handle recovers
     assert r["rc"] in (0, 1)
+    # ... exactly: the step results published after the refused solve (world 1:
+    # by the step kernels themselves) are this solve's, as a second solve shows
+    plan = shard.plan.cpu().numpy().copy()
+    r2 = rccl_solver.dist_solve_dev(shard, 0, a.N)
+    assert np.array_equal(shard.plan.cpu().numpy(), plan)
+    for key in ("objective", "utility", "makespan", "p2_objective", "bound", "iters", "status", "rc"):
+        assert r2[key] == r[key] or (r2[key] != r2[key] and r[key] != r[key]), key
 
 
 def test_gpu_shard_peer_transport_two_processes(tmp_path, shard_lib):
