@@ -67,7 +67,6 @@
 
 __device__ __forceinline__ uint32_t pk_r(uint32_t s) { return s & 0xFFu; }
 __device__ __forceinline__ uint32_t pk_w(uint32_t s) { return (s >> 8) & 0xFFu; }
-__device__ __forceinline__ uint32_t pk_sel(uint32_t s) { return (s >> 16) & 1u; }
 
 /* LDS the round loop needs: the running histogram's copies Hc; H and SH are
  * spare (kept for the carve-up of sw_kernels.hip). */
@@ -196,6 +195,12 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
         if (st[i] != 0u) atomicAdd(&Hm[pk_r(st[i])], (int32_t)pk_w(st[i]));
     __syncthreads();
     if (tid < 64) sw_pack_cum(L); /* the first round's barrier publishes it */
+    /* here st[i] = r | w << 8 | ra << 16, ra = r while the position is open
+     * this round and 0 once taken (as in the one-wave loop): with m < R,
+     * min(r, R) > m is r > m, so every eligibility test is one compare of ra */
+#define PK_RA(x) ((int32_t)(((x) >> 16) & 0xFFu))
+#pragma unroll
+    for (int i = 0; i < E; ++i) st[i] = (st[i] & 0xFFFFu) | ((st[i] & 0xFFu) << 16);
     SWP_STAMP(0);
     for (int t = 0; t < T; ++t) {
         const int R = T - t;
@@ -216,20 +221,16 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             const int32_t q = __builtin_amdgcn_readlane(need, m) - red;
             int32_t lt = 0;
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                const int rr = min((int)pk_r(st[i]), R);
-                lt += (!pk_sel(st[i]) && rr > m) ? (int32_t)pk_w(st[i]) : 0;
-            }
+            for (int i = 0; i < E; ++i) lt += PK_RA(st[i]) > m ? (int32_t)pk_w(st[i]) : 0;
             int32_t tot;
             int32_t ex = blk.exscan(lt, tot);
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
-                const int rr = min((int)pk_r(st[i]), R);
                 const int32_t w = (int32_t)pk_w(st[i]);
-                const bool elig = !pk_sel(st[i]) && rr > m;
+                const bool elig = PK_RA(st[i]) > m;
                 const bool take = elig && ex < q && ex + w <= cap;
-                st[i] |= take ? (1u << 16) : 0u;
+                st[i] = take ? (st[i] & 0xFFFFu) : st[i];
                 took += take ? w : 0;
                 ex += elig ? w : 0;
             }
@@ -243,17 +244,16 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
         {
             int32_t lt = 0;
 #pragma unroll
-            for (int i = 0; i < E; ++i)
-                lt += (!pk_sel(st[i]) && pk_r(st[i]) > 0) ? (int32_t)pk_w(st[i]) : 0;
+            for (int i = 0; i < E; ++i) lt += PK_RA(st[i]) > 0 ? (int32_t)pk_w(st[i]) : 0;
             int32_t tot;
             int32_t ex = blk.exscan(lt, tot);
             int32_t took = 0;
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 const int32_t w = (int32_t)pk_w(st[i]);
-                const bool elig = !pk_sel(st[i]) && pk_r(st[i]) > 0;
+                const bool elig = PK_RA(st[i]) > 0;
                 const bool take = elig && ex + w <= cap;
-                st[i] |= take ? (1u << 16) : 0u;
+                st[i] = take ? (st[i] & 0xFFFFu) : st[i];
                 took += take ? w : 0;
                 ex += elig ? w : 0;
             }
@@ -266,8 +266,7 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             int32_t best = 0x7FFFFFFF;
 #pragma unroll
             for (int i = E - 1; i >= 0; --i) {
-                const bool ok = !pk_sel(st[i]) && pk_r(st[i]) > 0 &&
-                                (int32_t)pk_w(st[i]) <= cap;
+                const bool ok = PK_RA(st[i]) > 0 && (int32_t)pk_w(st[i]) <= cap;
                 best = ok ? (((E * tid + i) << 8) | (int32_t)pk_w(st[i])) : best;
             }
             best = blk.min32(best);
@@ -275,22 +274,27 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
             if (best == 0x7FFFFFFF) break;
             const int pos = best >> 8;
 #pragma unroll
-            for (int i = 0; i < E; ++i) st[i] |= (E * tid + i == pos) ? (1u << 16) : 0u;
+            for (int i = 0; i < E; ++i) st[i] = (E * tid + i == pos) ? (st[i] & 0xFFFFu) : st[i];
             cap -= best & 0xFF;
         }
         SWP_STAMP(4);
         /* apply (all reads of the copies this round happened before the
-         * fill's barrier): placed positions move their width down one bin */
+         * fill's barrier): placed positions (r > 0, ra = 0) move their width
+         * down one bin and open for the next round with ra = r − 1 */
 #pragma unroll
         for (int i = 0; i < E; ++i) {
-            const bool sel = pk_sel(st[i]) != 0; /* only existing positions get selected */
             const uint32_t r = pk_r(st[i]);
+            const bool sel = PK_RA(st[i]) == 0 && r > 0;
             mk[i] |= sel ? (1ull << t) : 0ull;
-            st[i] = sel ? ((st[i] & 0xFF00u) | (r - 1u)) : st[i];
             if (sel) atomicAdd(&Hm[r], -(int32_t)pk_w(st[i])); /* C[r] alone */
+            const uint32_t r2 = r - (sel ? 1u : 0u);
+            st[i] = r2 | (st[i] & 0xFF00u) | (r2 << 16);
         }
         SWP_STAMP(5);
     }
+#pragma unroll
+    for (int i = 0; i < E; ++i) st[i] &= 0xFFFFu; /* r | w << 8, as the callers read it */
+#undef PK_RA
     SWP_FLUSH;
     __syncthreads();
 }
