@@ -2290,8 +2290,17 @@ int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     auto* S = (sw_shard_state*)ctx;
     SH_TRY(zero_red(S, 1));
     SH_TRY(arm_pub(S, S->dv.red, 8));
+    const bool early = S->dv.pub.dst != nullptr && S->P <= 64 * SW_BLOCK; /* world 1, a placement pack_any runs */
     LAUNCH(S, k_load, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p);
     disarm_pub(S);
+    if (early) {
+        /* world 1: the share is G in every round whenever there is one
+         * (sw_share_caps), so the placement is enqueued before the host waits
+         * for the load; a load that allows no share placement has its rows
+         * cleared below, after it in stream order */
+        for (int32_t t = 0; t < S->T; ++t) S->scaps[t] = S->dv.G;
+        SH_TRY(pack_any(S, 4, src, 0.0, ydst, pdst, 0, S->scaps, true));
+    }
     std::vector<int64_t> loads((size_t)S->world);
     SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 8, loads.data()));
     S->share = sw_share_caps(loads.data(), S->world, S->rank, S->T, S->dv.G, S->scaps) == 0;
@@ -2300,6 +2309,7 @@ int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
         SH_HIP(S, hipMemsetAsync(S->arr[pdst].p, 0, (size_t)S->NL * 4, S->h->stream));
         return SW_OK;
     }
+    if (early) return SW_OK; /* placed above, with these caps */
     return pack_any(S, 4, src, 0.0, ydst, pdst, 0, S->scaps, true);
 }
 
