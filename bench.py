@@ -327,6 +327,9 @@ def main():
     batch = [ss.synth_problem(args.seed + rank * 100_000 + i, args.jobs, 256, args.rounds, 120.0,
                               1e5, 5.0) for i in range(args.batch)]
     solver.upload(batch)
+    # the plan bytes are the solve's output (shockwave.py:390-398 reads x[j][t]);
+    # the bit-packed copy (plan_masks) is stored only for callers that ask
+    solver.keep_masks(False)
 
     def barrier():
         torch.cuda.synchronize()

@@ -183,6 +183,16 @@ int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* problems);
 int sw_batch_run(sw_handle* h);
 int sw_batch_download(sw_handle* h, sw_result* results);
 
+/*
+ * Whether sw_batch_run also stores the bit-packed plans (plan_masks, 8 bytes
+ * per job in HBM) besides the plan bytes: keep = 1 (the default) or 0.  With
+ * 0 the kernels skip those stores, and sw_batch_download of a run made so
+ * refuses a result that asks for plan_masks (SW_ERR_INVALID).  The
+ * host-buffer entry points (sw_plan_solve, sw_plan_solve_batch) decide from
+ * their own results' plan_masks and ignore this setting.
+ */
+int sw_batch_keep_masks(sw_handle* h, int32_t keep);
+
 /* The HIP stream the handle launches on (hipStream_t as void*). */
 void* sw_stream(sw_handle* h);
 
@@ -191,11 +201,11 @@ void* sw_stream(sw_handle* h);
  * each launch of sw_batch_run.  enable=1 turns it on (adds two event records
  * per kernel).  sw_kernel_times() synchronises and returns accumulated ms for
  * [0] the P2 exchange kernel (sw_p2x_kernel) and [1] the plan kernels
- * (sw_plan_kernel, or the split level / pack / slow-path kernels of batches
- * above 1,024 on-chip instances), plus the number of runs.  On-chip batches
- * of at most 256 instances (every single solve) run the exchange step fused
- * at the end of sw_plan_kernel: there [0] reads 0 and [1] holds both, so
- * the two stages are not separable.
+ * (sw_plan_kernel, or the split level / pack / slow-path kernels of large
+ * on-chip batches), plus the number of runs.  Wherever the exchange step runs
+ * fused inside the plan kernels — every on-chip batch of at most 256
+ * instances (every single solve) and every split batch — [0] reads 0 and [1]
+ * holds both stages, which are then not separable.
  */
 int sw_set_timing(sw_handle* h, int32_t enable);
 int sw_kernel_times(sw_handle* h, double* ms_p2x, double* ms_plan, int32_t* runs);

@@ -448,9 +448,10 @@ int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
 /* The solve kernels for instances [lo, hi) of the loaded batch on s: the
  * per-instance arrays offset to lo, the per-job ones global (each
  * descriptor holds its global job and plan offsets). */
-int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
+int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed, bool want_masks) {
     sw_batch_dev B;
     memset(&B, 0, sizeof(B));
+    B.want_masks = want_masks ? 1 : 0;
     B.inst = h->d_inst + lo;
     B.count = hi - lo;
     B.KT = h->maxT <= 32 ? 32 : 64;
@@ -483,16 +484,19 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed) {
         if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
         SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], s));
     }
-    /* large on-chip batches: level-search kernel, pack kernel, full kernel
-     * for the instances the pack kernel leaves (sw_kernels.hip), then the
-     * exchange kernel; on-chip batches of at most one instance per CU: the
-     * full kernel with the exchange step fused at its end (one launch; each
-     * CU runs its instance's solve and exchange back to back, instead of
-     * every exchange waiting for the batch's slowest solve); otherwise the
-     * full kernel, then the exchange kernel (at two or more instances per
-     * CU the fused form would serialise a CU's exchanges behind its solves,
-     * where the exchange kernel runs four per CU: C5's 512 instances take
-     * 2.03 ms fused against 1.93 ms, profiles/r3w_c5_stages.json) */
+    /* Dispatch.  On-chip batches (every N ≤ SW_LDS_JOBS, T ≤ 32) above
+     * split_min_count() instances: the level-search kernel, then the pack
+     * kernel — each instance's P2 exchange step runs at its end, in the same
+     * workgroup — then the full kernel for the instances the pack kernel
+     * marked, with their exchange steps fused at its end too
+     * (sw_launch_split).  Smaller on-chip batches of at most fuse_max_count()
+     * instances: the full kernel with the exchange fused at its end.  The
+     * rest (larger on-chip batches below the split size, and every batch with
+     * an instance above SW_LDS_JOBS jobs or 32 rounds): the full kernel, then
+     * the exchange kernel (sw_p2x_kernel.hip).  Timing: with the exchange
+     * fused, the plan events bracket both stages and the exchange events an
+     * empty interval, so sw_kernel_times reports the exchange inside the plan
+     * time (include/shockwave_amd.h sw_set_timing). */
 #ifdef SW_STAMPS
     const bool split = false; /* diagnostic builds time the phases inside the full kernel */
 #else
@@ -626,7 +630,7 @@ int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_res
         if ((err = h2d(h, cut[c], cut[c + 1], h->up)) != SW_OK) break;
         SW_HIP(h, hipEventRecord(e_up, h->up));
         SW_HIP(h, hipStreamWaitEvent(h->stream, e_up, 0));
-        if ((err = launch(h, cut[c], cut[c + 1], h->stream, false)) != SW_OK) break;
+        if ((err = launch(h, cut[c], cut[c + 1], h->stream, false, w.masks)) != SW_OK) break;
         SW_HIP(h, hipEventRecord(e_k, h->stream));
         SW_HIP(h, hipStreamWaitEvent(h->dn, e_k, 0));
         if ((err = d2h(h, cut[c], cut[c + 1], h->dn, w)) != SW_OK) break;
@@ -685,7 +689,14 @@ int sw_batch_run(sw_handle* h) {
     if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
     if (h->count <= 0) return SW_OK;
     SW_HIP(h, hipSetDevice(h->device));
-    return launch(h, 0, h->count, h->stream, h->timing);
+    h->masks_valid = h->keep_masks;
+    return launch(h, 0, h->count, h->stream, h->timing, h->keep_masks);
+}
+
+int sw_batch_keep_masks(sw_handle* h, int32_t keep) {
+    if (!h) return SW_ERR_INVALID;
+    h->keep_masks = keep != 0;
+    return SW_OK;
 }
 
 int sw_batch_download(sw_handle* h, sw_result* res) {
@@ -693,7 +704,10 @@ int sw_batch_download(sw_handle* h, sw_result* res) {
     if (!h->loaded) return fail(h, SW_ERR_INVALID, "no batch uploaded");
     if (h->count > 0 && !res) return fail(h, SW_ERR_INVALID, "null result array");
     SW_HIP(h, hipSetDevice(h->device));
-    int rc = d2h(h, 0, h->count, h->stream, wants_of(res, h->count));
+    const Wants w = wants_of(res, h->count);
+    if (w.masks && !h->masks_valid)
+        return fail(h, SW_ERR_INVALID, "plan_masks: the last sw_batch_run did not keep them (sw_batch_keep_masks)");
+    int rc = d2h(h, 0, h->count, h->stream, w);
     if (rc != SW_OK) return rc;
     SW_HIP(h, hipStreamSynchronize(h->stream));
     if (collect_timing(h) != SW_OK) return SW_ERR_HIP;
@@ -723,8 +737,12 @@ int sw_plan_solve_batch(sw_handle* h, int32_t count, const sw_problem* probs, sw
 #endif
     int rc = sw_batch_upload(h, count, probs);
     if (rc < 0) return rc;
-    rc = sw_batch_run(h);
-    if (rc < 0) return rc;
+    if (count > 0) { /* sw_batch_run, keeping the masks only if asked for */
+        const bool km = wants_of(res, count).masks;
+        SW_HIP(h, hipSetDevice(h->device));
+        h->masks_valid = km;
+        if ((rc = launch(h, 0, h->count, h->stream, h->timing, km)) < 0) return rc;
+    }
     return sw_batch_download(h, res);
 }
 

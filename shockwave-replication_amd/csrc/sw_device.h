@@ -80,5 +80,7 @@ struct sw_batch_dev {
     sw_ws_dev ws;
     unsigned char* p2ws; /* P2 exchange arrays, SW_P2X_ARR_BYTES per job (sw_p2x_inst.h) */
     int32_t fuse_p2x;    /* sw_plan_kernel: run the exchange step after the solve (sw_p2x_inst.h) */
+    int32_t want_masks;  /* sw_pack_kernel: store the final masks (a caller asked for plan_masks) */
+    int32_t lds_bytes;   /* sw_pack_kernel: its dynamic LDS allocation (the exchange arrays' room) */
     uint64_t* stamps; /* diagnostic builds only (SW_STAMPS): [count][SW_STAMP_SLOTS] cycles (8…13: pack round-loop phases, 16…: level search, 32…: exchange) */
 };

@@ -64,6 +64,8 @@ struct sw_handle {
     std::string err;
     /* batch description (host) */
     bool loaded = false; /* a batch upload completed (run / download need one) */
+    bool keep_masks = true;   /* sw_batch_run stores plan_masks (sw_batch_keep_masks) */
+    bool masks_valid = false; /* the last run stored them */
     int32_t count = 0;
     int64_t total_jobs = 0;
     int64_t total_plan = 0;

@@ -1706,7 +1706,9 @@ __device__ __forceinline__ void emit_plan_bytes(uint8_t* plan, const uint64_t* y
  * constants, no key rows: ~47 KB of LDS and ≤ 80 VGPRs, so three instances
  * share a CU.
  */
-__device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned char* smem, int inst_) {
+/* Returns the instance's final placement (the masks, in LDS) for the tail
+ * below, or nullptr when the instance was left to sw_plan_kernel. */
+__device__ __forceinline__ const uint64_t* pack_instance(const sw_batch_dev& B, unsigned char* smem, int inst_) {
     const sw_inst_dev* I = &B.inst[inst_];
     Ctx<32, true, true> c;
     c.inst = I;
@@ -1720,7 +1722,6 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     const sw_lvl_dev lv = B.lvl[inst_];
     c.passes = lv.passes;
     c.q = (c.N + SW_BLOCK - 1) / SW_BLOCK;
-    const int N = c.N, T = c.T;
     const int64_t jo = I->job_off;
     c.w_in = B.w + jo;
     c.p_in = B.p + jo;
@@ -1769,7 +1770,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     sw_out_dev* out = &B.out[inst_];
     if (c.blk.sum(act_l) > SW_BLOCK) { /* more positions than threads: sw_plan_kernel */
         if (threadIdx.x == 0) out->status = SW_STATUS_SLOW_MARK;
-        return;
+        return nullptr;
     }
     /* twin_plan_solve's first pack: the density order (mode 4) */
     c.pack(4, c.nbest, c.ycur, c.placed);
@@ -1792,7 +1793,7 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
     }
     if (dfc != 0) { /* the other P1 orders, re-solves, fill: sw_plan_kernel */
         if (threadIdx.x == 0) out->status = SW_STATUS_SLOW_MARK;
-        return;
+        return nullptr;
     }
     /* emit (solve_instance's, with the level search's U and M) */
     int64_t any_l = 0;
@@ -1814,7 +1815,6 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
         }
         p2 = p2 + term;
         B.planned[jo + j] = cnt;
-        B.masks[jo + j] = m;
     });
     const double P2 = c.blk.detsum(p2);
     const int64_t any_n = c.blk.sum(any_l); /* its barrier: every mask row is final */
@@ -1832,7 +1832,123 @@ __device__ __forceinline__ void pack_instance(const sw_batch_dev& B, unsigned ch
         o.status = status | (sw_p1_uncertified(o.objective, lv.bound) ? SW_STATUS_P1_UNCERTIFIED : 0);
         *out = o;
     }
-    emit_plan_bytes(B.plan + I->plan_off, c.ycur, N, T);
+    return c.ycur; /* the plan bytes and masks: after the exchange step (pack_tail) */
+}
+
+/*
+ * The pack kernel's tail: the instance's P2 exchange step (sw_p2x_block,
+ * DESIGN.md §3.6) on the placement ym the pack left in LDS, then the plan
+ * bytes — stored once, from the final masks — and the masks themselves only
+ * when a caller asked for them (B.want_masks).  The masks go to registers
+ * first (thread l holds jobs [l·q, l·q + q), q ≤ 2 on chip), so the step may
+ * reuse every byte of LDS; its 24-byte-per-job arrays go to LDS behind the
+ * step's own state when the launch's allocation (B.lds_bytes) holds them, and
+ * to the HBM workspace otherwise.  The same step on the same arrays as
+ * sw_p2x_instance (sw_p2x_inst.h), so the same masks and P2 bits; it only
+ * moves where the arrays live and drops the mask round trip through HBM
+ * (written back from L2 for every instance of the batch).
+ */
+__device__ __forceinline__ void pack_tail(const sw_batch_dev& B, const uint64_t* ym, unsigned char* smem,
+                                          int inst) {
+    const sw_inst_dev* I = &B.inst[inst];
+    sw_out_dev* out = &B.out[inst];
+    const int N = I->N, T = I->T, G = I->G;
+    const int64_t jo = I->job_off;
+    const int q = (N + SW_BLOCK - 1) / SW_BLOCK; /* ≤ 2: N ≤ SW_LDS_JOBS */
+    const int j0 = (int)threadIdx.x * q, j1 = min(j0 + q, N);
+    __syncthreads(); /* the emit's status and ym are final; the pack's reductions are read */
+    int act = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) act += (j0 + k < j1 && ym[j0 + k] != 0ull) ? 1 : 0;
+    const bool run = B.fuse_p2x && !(out->status & SW_STATUS_P2_FALLBACK);
+    sw_p2x_lds* L = reinterpret_cast<sw_p2x_lds*>(smem);
+    const size_t Lsz = (sizeof(sw_p2x_lds) + 15) & ~(size_t)15;
+    unsigned char* var = smem + Lsz;
+    sw_blk blk;
+    blk.X = &L->X;
+    blk.par = 0;
+    int A = 0;
+    const int a0 = blk.exscan(act, A);
+    A = __builtin_amdgcn_readfirstlane(A); /* uniform: the arrays' addresses stay scalar through the step */
+    const uint64_t* yemit = ym; /* no step: ym is untouched (only blk.X was written) */
+    if (run && A > 0 && A <= SW_P2X_AMAX) {
+        /* the arrays in LDS behind the step's state when the allocation holds
+         * them and they start past ym (read below while they are written) */
+        const size_t vb = (sw_p2x_var_bytes(A, T) + 15) & ~(size_t)15;
+        const bool onchip = Lsz + vb + (size_t)SW_P2X_ARR_BYTES * A <= (size_t)B.lds_bytes &&
+                            var + vb >= reinterpret_cast<const unsigned char*>(ym + N);
+        unsigned char* base = onchip ? var + vb : B.p2ws + (size_t)SW_P2X_ARR_BYTES * jo;
+        const size_t n = onchip ? (size_t)A : (size_t)N;
+        sw_p2x_arrays X;
+        X.cc = reinterpret_cast<double*>(base);
+        X.cm = reinterpret_cast<uint64_t*>(X.cc + n);
+        X.cw = reinterpret_cast<int32_t*>(X.cm + n);
+        X.cj = X.cw + n;
+        for (int k = 0, a = a0; k < 2; ++k) {
+            if (j0 + k >= j1) break;
+            const uint64_t m = ym[j0 + k];
+            if (m == 0ull) continue;
+            const int j = j0 + k;
+            X.cw[a] = B.w[jo + j];
+            X.cj[a] = j;
+            X.cc[a] = B.p[jo + j] / (double)__popcll(m);
+            X.cm[a] = m;
+            ++a;
+        }
+        __syncthreads();
+#ifdef SW_STAMPS
+        uint64_t* sp = B.stamps ? B.stamps + (size_t)inst * SW_STAMP_SLOTS + 32 : nullptr;
+#else
+        uint64_t* sp = nullptr;
+#endif
+        const int nc = sw_p2x_block<SW_WAVES>(blk, L, var, X, A, T, G, sp);
+        __syncthreads(); /* the cancels' mask updates */
+        /* the final masks: this thread's active jobs (count > 0, unchanged by
+         * the step: B.planned) in compaction order, the offsets counted again
+         * rather than kept live through the step */
+        int act2 = 0;
+        for (int j = j0r(N); j < j1r(N); ++j) act2 += B.planned[jo + j] > 0;
+        int A2;
+        int a = blk.exscan(act2, A2);
+        uint64_t mf[2];
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int j = j0r(N) + k;
+            mf[k] = 0ull;
+            if (j >= j1r(N)) continue;
+            if (B.planned[jo + j] <= 0) {
+                acc = acc + 0.0;
+                continue;
+            }
+            mf[k] = X.cm[a++];
+            const int cnt = __popcll(mf[k]);
+            const int64_t Ssum = (int64_t)__popcll(mf[k] & 0xAAAAAAAAAAAAAAAAull) +
+                                 2 * (int64_t)__popcll(mf[k] & 0xCCCCCCCCCCCCCCCCull) +
+                                 4 * (int64_t)__popcll(mf[k] & 0xF0F0F0F0F0F0F0F0ull) +
+                                 8 * (int64_t)__popcll(mf[k] & 0xFF00FF00FF00FF00ull) +
+                                 16 * (int64_t)__popcll(mf[k] & 0xFFFF0000FFFF0000ull) +
+                                 32 * (int64_t)__popcll(mf[k] & 0xFFFFFFFF00000000ull);
+            acc = acc + ((double)Ssum / (double)cnt) * B.p[jo + j];
+        }
+        if (nc > 0) { /* the P2 objective of the final masks, summed like the emit's */
+            const double P2 = blk.detsum(acc);
+            if (threadIdx.x == 0) {
+                out->p2_objective = P2;
+                out->status |= SW_STATUS_P2_EXCHANGED;
+            }
+        }
+        __syncthreads(); /* every read of the step's LDS (and blk.X) is done: the masks go to offset 0 */
+        uint64_t* yf = reinterpret_cast<uint64_t*>(smem);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (j0r(N) + k < j1r(N)) yf[j0r(N) + k] = mf[k];
+        yemit = yf;
+        __syncthreads();
+    }
+    if (B.want_masks)
+        for (int j = j0r(N); j < j1r(N); ++j) B.masks[jo + j] = yemit[j];
+    emit_plan_bytes(B.plan + I->plan_off, yemit, N, T);
 }
 
 /* The re-optimisation's view of an instance (sw_reround_dev.h): the best P1
@@ -2370,11 +2486,8 @@ __global__ __launch_bounds__(SW_BLOCK, 4) void sw_level_kernel(sw_batch_dev B) {
  * first and all the exchanges after them. */
 __global__ __launch_bounds__(SW_BLOCK, 8) void sw_pack_kernel(sw_batch_dev B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sw_smem[];
-    pack_instance(B, sw_smem, blockIdx.x);
-    if (B.fuse_p2x) {
-        __syncthreads(); /* the emit's masks and status are visible */
-        if (!(B.out[blockIdx.x].status & SW_STATUS_SLOW_MARK)) sw_p2x_instance(B, B.p2ws, sw_smem, blockIdx.x);
-    }
+    const uint64_t* ym = pack_instance(B, sw_smem, blockIdx.x);
+    if (ym) pack_tail(B, ym, sw_smem, blockIdx.x); /* uniform: marked instances return */
 }
 
 /* LDS bytes the kernel needs (solve_instance checks its carve-up against it). */
@@ -2391,7 +2504,8 @@ extern "C" hipError_t sw_launch_split(sw_batch_dev* B, size_t p2x_lds, hipStream
     B->only_slow = 0;
     B->fuse_p2x = 1;
     hipLaunchKernelGGL((sw_level_kernel<32>), grid, block, sw_level_lds_bytes(), stream, *B);
-    hipLaunchKernelGGL(sw_pack_kernel, grid, block, std::max(sw_pack_lds_bytes(), p2x_lds), stream, *B);
+    B->lds_bytes = (int32_t)std::max(sw_pack_lds_bytes(), p2x_lds);
+    hipLaunchKernelGGL(sw_pack_kernel, grid, block, (size_t)B->lds_bytes, stream, *B);
     B->only_slow = 1;
     hipLaunchKernelGGL((sw_plan_kernel<32, true>), grid, block, std::max(sw_plan_lds_bytes(true), p2x_lds),
                        stream, *B);

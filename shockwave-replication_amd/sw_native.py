@@ -317,7 +317,7 @@ EXPORTED_SYMBOLS = (
     "sw_batch_download", "sw_stream", "sw_set_timing", "sw_kernel_times",
     "sw_dist_unique_id", "sw_dist_init", "sw_dist_plan_solve", "sw_dist_shard_range",
     "sw_dist_init_host", "sw_mmf_allocate", "sw_dist_plan_solve_dev", "sw_dist_enable_peer",
-    "sw_mmf_allocate_types",
+    "sw_mmf_allocate_types", "sw_batch_keep_masks",
 )
 
 
@@ -364,6 +364,8 @@ def load(path: str | None = None):
     lib.sw_batch_run.restype = C.c_int
     lib.sw_batch_download.argtypes = [C.c_void_p, C.POINTER(SwResult)]
     lib.sw_batch_download.restype = C.c_int
+    lib.sw_batch_keep_masks.argtypes = [C.c_void_p, C.c_int32]
+    lib.sw_batch_keep_masks.restype = C.c_int
     lib.sw_stream.argtypes = [C.c_void_p]
     lib.sw_stream.restype = C.c_void_p
     lib.sw_set_timing.argtypes = [C.c_void_p, C.c_int32]
@@ -468,10 +470,25 @@ class Solver:
     def run(self):
         self._check(self.lib.sw_batch_run(self.h), "sw_batch_run")
 
-    def download(self) -> list:
+    def keep_masks(self, keep: bool):
+        """sw_batch_keep_masks: whether sw_batch_run stores the bit-packed plans."""
+        self._check(self.lib.sw_batch_keep_masks(self.h, 1 if keep else 0), "sw_batch_keep_masks")
+
+    def download(self, masks: bool = False) -> list:
+        """sw_batch_download; masks=True also asks for the bit-packed plans
+        ("plan_masks", which the last run must have kept: keep_masks)."""
         ress = (SwResult * len(self._batch))(*[a.c_result() for a in self._batch])
+        mk = []
+        if masks:
+            for i, a in enumerate(self._batch):
+                m = np.zeros(max(a.N, 1), dtype=np.uint64)
+                ress[i].plan_masks = m.ctypes.data_as(C.POINTER(C.c_uint64))
+                mk.append(m)
         rc = self._check(self.lib.sw_batch_download(self.h, ress), "sw_batch_download")
-        return [result_dict(ress[i], a, rc) for i, a in enumerate(self._batch)]
+        out = [result_dict(ress[i], a, rc) for i, a in enumerate(self._batch)]
+        for d, m, a in zip(out, mk, self._batch):
+            d["plan_masks"] = m[:a.N]
+        return out
 
     def stream(self) -> int:
         return self.lib.sw_stream(self.h) or 0

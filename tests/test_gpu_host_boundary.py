@@ -105,3 +105,29 @@ def test_gpu_pipelined_batch_with_empty_instances_and_no_outputs(gpu_solver, twi
     for i in range(0, 4608, 7):
         assert cr[i].objective == rb[i]["objective"] and cr[i].status == rb[i]["status"], i
         assert cr[i].p2_objective == rb[i]["p2_objective"], i
+
+
+def test_gpu_resident_split_batch_keep_masks(gpu_solver, twin):
+    """The split kernels' pack tail (sw_kernels.hip pack_tail: the exchange
+    step's arrays in LDS, the masks stored only when kept): a 600-instance
+    device-resident batch gives the same plans and results with and without
+    the masks, the kept masks are the plan bytes packed, and a download that
+    asks for masks after a run that did not keep them is refused."""
+    import sw_native as sn
+
+    probs = onchip(600, 350_000)
+    gpu_solver.upload(probs)
+    gpu_solver.keep_masks(True)
+    gpu_solver.run()
+    with_m = gpu_solver.download(masks=True)
+    gpu_solver.keep_masks(False)
+    gpu_solver.run()
+    without = gpu_solver.download()
+    with pytest.raises(sn.NativeError, match="plan_masks"):
+        gpu_solver.download(masks=True)
+    gpu_solver.keep_masks(True)
+    for i, (a, m, n) in enumerate(zip(probs, with_m, without)):
+        assert_same_result(m, n, f"case {i}")
+        assert np.array_equal(m["plan_masks"], pack_bits(m["plan"])), f"case {i}"
+    for i in range(0, len(probs), 5):
+        assert_same_result(without[i], twin.solve(probs[i]), f"case {i} vs twin")
