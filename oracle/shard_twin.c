@@ -47,7 +47,7 @@ typedef struct {
     int32_t* arr[SW_A_COUNT];
     uint64_t* y[SW_Y_COUNT];
     int32_t* w_all;
-    int32_t scaps[SW_TMAX]; /* this rank's share of every round (pack_share) */
+    int32_t scaps[SW_VSHARES][SW_TMAX]; /* this rank's shares of every round (pack_share) */
     int share;              /* the shares exist (sw_share_caps succeeded) */
     sw_result* res;
 } eng_t;
@@ -435,16 +435,34 @@ static int e_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_
     return 0;
 }
 
-/* the share placement (sw_shard_ops.pack_share): loads all-gathered, this
- * rank's jobs packed alone into its shares of the rounds (density order,
- * mixed widths, the tier rule over non-uniform capacities: plan_twin.c pack) */
+/* this rank's shares (sw_share_count): S = V / W of them, share s holding the
+ * local jobs [lo, hi) */
+static int32_t e_shares(const eng_t* E, int32_t s, int32_t* lo, int32_t* hi) {
+    const int32_t V = sw_share_count(E->N, E->G, E->world), S = V / E->world;
+    int64_t a = 0, b = 0;
+    if (s < S) sw_shard_range(E->N, V, E->rank * S + s, &a, &b);
+    *lo = (int32_t)(a - E->off);
+    *hi = (int32_t)(b - E->off);
+    return S;
+}
+
+/* the share placement (sw_shard_ops.pack_share): the loads of every share
+ * all-gathered, this rank's jobs of each of its shares packed alone into that
+ * share of the rounds (density order, mixed widths, the tier rule over
+ * non-uniform capacities: plan_twin.c pack) */
 static int e_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     eng_t* E = (eng_t*)ctx;
     const int32_t NL = E->NL, T = E->T;
     const size_t NN = NL > 0 ? (size_t)NL : 1;
-    int64_t mine = 0;
-    for (int32_t i = 0; i < NL; ++i) mine += (int64_t)E->jc[i].w * E->arr[src][i];
-    int64_t* loads = (int64_t*)calloc((size_t)E->world, sizeof(int64_t));
+    int32_t lo, hi;
+    const int32_t S = e_shares(E, 0, &lo, &hi), V = S * E->world;
+    int64_t mine[SW_VSHARES];
+    for (int32_t s = 0; s < S; ++s) {
+        e_shares(E, s, &lo, &hi);
+        mine[s] = 0;
+        for (int32_t i = lo; i < hi; ++i) mine[s] += (int64_t)E->jc[i].w * E->arr[src][i];
+    }
+    int64_t* loads = (int64_t*)calloc((size_t)V, sizeof(int64_t));
     int32_t* w = (int32_t*)malloc(sizeof(int32_t) * NN);
     int32_t* nin = (int32_t*)malloc(sizeof(int32_t) * NN);
     uint64_t* k1 = (uint64_t*)malloc(sizeof(uint64_t) * NN);
@@ -453,15 +471,23 @@ static int e_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     uint8_t* y = (uint8_t*)calloc(NN * (size_t)T, 1);
     int rc = -1;
     if (!loads || !w || !nin || !k1 || !k2 || !placed || !y) goto out;
-    rc = E->comm->allgather(E->comm->ctx, &mine, loads, (int64_t)sizeof(int64_t));
+    rc = E->comm->allgather(E->comm->ctx, mine, loads, (int64_t)sizeof(int64_t) * S);
     if (rc) goto out;
-    E->share = sw_share_caps(loads, E->world, E->rank, T, E->G, E->scaps) == 0;
+    E->share = 1;
+    for (int32_t s = 0; s < S; ++s)
+        E->share &= sw_share_caps(loads, V, E->rank * S + s, T, E->G, E->scaps[s]) == 0;
     for (int32_t i = 0; i < NL; ++i) {
         w[i] = E->jc[i].w;
         nin[i] = E->share ? E->arr[src][i] : 0;
         k1[i] = nin[i] > 0 ? sw_ratio_key(E->p[i] / (double)(nin[i] * w[i])) : 0;
     }
-    if (E->share) twin_pack_arrays_caps(NL, T, E->G, w, nin, k1, k2, y, placed, E->scaps, 0);
+    if (E->share)
+        for (int32_t s = 0; s < S; ++s) {
+            e_shares(E, s, &lo, &hi);
+            if (hi > lo)
+                twin_pack_arrays_caps(hi - lo, T, E->G, w + lo, nin + lo, k1 + lo, k2 + lo,
+                                      y + (size_t)lo * T, placed + lo, E->scaps[s], 0);
+        }
     for (int32_t i = 0; i < NL; ++i) {
         uint64_t m = 0;
         for (int32_t t = 0; t < T; ++t) m |= (uint64_t)y[(size_t)i * T + t] << t;
@@ -473,23 +499,22 @@ out:
     return rc;
 }
 
-/* sw_shard_ops.share_repair: when this rank's share pack stranded rounds,
- * its width profile is repaired inside its shares (sw_profile_repair with
- * the shares' free GPUs) and every changed class is repacked alone (unit
- * widths, order p/n) — plan_twin.c repair_pack on the rank's own jobs */
-static int e_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
-    eng_t* E = (eng_t*)ctx;
-    const int32_t NL = E->NL, T = E->T;
-    if (!E->share) return 0;
+/* sw_shard_ops.share_repair: every share of this rank whose pack stranded
+ * rounds has its width profile repaired inside the share (sw_profile_repair
+ * with the share's free GPUs) and every changed class repacked alone (unit
+ * widths, order p/n) — plan_twin.c repair_pack on the share's own jobs */
+static int e_share_repair_one(eng_t* E, int32_t src, int32_t ydst, int32_t pdst, int32_t lo, int32_t hi,
+                              const int32_t* scaps) {
+    const int32_t T = E->T, NL = hi - lo;
     int64_t dfc = 0;
-    for (int32_t i = 0; i < NL; ++i) dfc += (int64_t)E->jc[i].w * (E->arr[src][i] - E->arr[pdst][i]);
+    for (int32_t i = lo; i < hi; ++i) dfc += (int64_t)E->jc[i].w * (E->arr[src][i] - E->arr[pdst][i]);
     if (dfc == 0) return 0;
     sw_repair_t R;
     memset(&R, 0, sizeof(R));
-    for (int32_t i = 0; i < NL; ++i)
+    for (int32_t i = lo; i < hi; ++i)
         if (E->arr[src][i] > 0 && sw_repair_add_class(&R, E->jc[i].w) < 0) return 0;
-    for (int32_t t = 0; t < T; ++t) R.L[t] = E->scaps[t];
-    for (int32_t i = 0; i < NL; ++i) {
+    for (int32_t t = 0; t < T; ++t) R.L[t] = scaps[t];
+    for (int32_t i = lo; i < hi; ++i) {
         const uint64_t m = E->y[ydst][i];
         for (int32_t t = 0; t < T; ++t)
             if ((m >> t) & 1u) R.L[t] -= E->jc[i].w;
@@ -509,27 +534,39 @@ static int e_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     uint8_t* yc = (uint8_t*)calloc(NN * (size_t)T, 1);
     int rc = -1;
     if (!w || !nc || !k1 || !k2 || !pc || !yc) goto out;
-    for (int32_t i = 0; i < NL; ++i) w[i] = E->jc[i].w;
+    for (int32_t i = 0; i < NL; ++i) w[i] = E->jc[lo + i].w;
     for (int32_t c = 0; c < R.ncls; ++c) {
         if (!R.changed[c]) continue;
         for (int32_t i = 0; i < NL; ++i) {
-            const int cls = E->arr[src][i] > 0 && w[i] == R.wc[c];
-            nc[i] = cls ? E->arr[src][i] : 0;
-            k1[i] = cls ? sw_ratio_key(E->p[i] / (double)nc[i]) : 0;
+            const int cls = E->arr[src][lo + i] > 0 && w[i] == R.wc[c];
+            nc[i] = cls ? E->arr[src][lo + i] : 0;
+            k1[i] = cls ? sw_ratio_key(E->p[lo + i] / (double)nc[i]) : 0;
         }
         twin_pack_arrays_caps(NL, T, E->G, w, nc, k1, k2, yc, pc, R.caps[c], 1);
         for (int32_t i = 0; i < NL; ++i) {
             if (nc[i] <= 0) continue;
             uint64_t m = 0;
             for (int32_t t = 0; t < T; ++t) m |= (uint64_t)yc[(size_t)i * T + t] << t;
-            E->y[ydst][i] = m;
-            E->arr[pdst][i] = pc[i];
+            E->y[ydst][lo + i] = m;
+            E->arr[pdst][lo + i] = pc[i];
         }
     }
     rc = 0;
 out:
     free(w); free(nc); free(k1); free(k2); free(pc); free(yc);
     return rc;
+}
+
+static int e_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
+    eng_t* E = (eng_t*)ctx;
+    if (!E->share) return 0;
+    int32_t lo, hi;
+    const int32_t S = e_shares(E, 0, &lo, &hi);
+    for (int32_t s = 0; s < S; ++s) {
+        e_shares(E, s, &lo, &hi);
+        if (e_share_repair_one(E, src, ydst, pdst, lo, hi, E->scaps[s]) < 0) return -1;
+    }
+    return 0;
 }
 
 /* the P2 exchange step on the gathered placement (twin_p2x_run) */

@@ -93,6 +93,12 @@ struct sw_pack_ent {
 struct ShardDev {
     int32_t NL, T, G, nb, LW, rank;
     int64_t off, N, q, P;
+    /* the share placement's shares on this rank (sw_share_count): nsub of
+     * them, share s holding the local jobs [s·Ps, (s + 1)·Ps) and its
+     * placement entries at [s·Pp, s·Pp + Ps) (Pp: Ps rounded up to the sort's
+     * chunk) */
+    int32_t nsub;
+    int64_t Ps, Pp;
     double k;
     double beta[SW_BMAX], ell[SW_BMAX], slope[SW_BMAX];
     const sw_jobc* jc;
@@ -688,13 +694,23 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
 /* this rank's entries (twin: the k1/k2 of each pack caller) */
 /* mode 1/3 P1 orders A/B, 2 P2 weight order, 4 P2 density order, 5 the
  * class-wise P2 repack of width wc (unit widths) */
+/* sub: the shares' layout (entry s·Pp + k = job s·Ps + k, padding zero);
+ * else entry i = job i of [0, P).  Jobs outside [jlo, jhi) take no entry. */
 __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const int32_t* src,
-                                                   double Mb, int wc, sw_pack_ent* out) {
-    const int i = blockIdx.x * kTB + threadIdx.x;
-    if (i >= S.P) return;
-    sw_pack_ent e;
-    e.khi = 0; e.klo = 0; e.st = 0; e.pad = 0;
-    if (i < S.NL) {
+                                                   double Mb, int wc, sw_pack_ent* out, int sub = 0,
+                                                   int jlo = 0, int jhi = 0x7FFFFFFF) {
+    const int e = blockIdx.x * kTB + threadIdx.x;
+    int64_t i = e;
+    if (sub) {
+        if (e >= (int64_t)S.nsub * S.Pp) return;
+        const int64_t sh = e / S.Pp, k = e - sh * S.Pp;
+        i = k < S.Ps ? sh * S.Ps + k : (int64_t)S.NL; /* padding: no job */
+    } else if (e >= S.P) {
+        return;
+    }
+    sw_pack_ent ent;
+    ent.khi = 0; ent.klo = 0; ent.st = 0; ent.pad = 0;
+    if (i < S.NL && i >= jlo && i < jhi) {
         const sw_jobc c = S.jc[i];
         const int n = (mode == 5 && c.w != wc) ? 0 : src[i];
         if (n > 0) {
@@ -712,12 +728,12 @@ __global__ __launch_bounds__(kTB) void k_pack_keys(ShardDev S, int mode, const i
                 k1 = sw_ratio_key(S.p[i] / (double)n);
                 k2 = 0;
             }
-            e.khi = k1;
-            e.klo = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(S.off + i));
-            e.st = (uint32_t)n | ((mode == 5 ? 1u : (uint32_t)c.w) << 8);
+            ent.khi = k1;
+            ent.klo = ((uint64_t)k2 << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)(S.off + i));
+            ent.st = (uint32_t)n | ((mode == 5 ? 1u : (uint32_t)c.w) << 8);
         }
     }
-    out[i] = e;
+    out[e] = ent;
 }
 
 /* width-class profile: red[t] = #{local j : src_j > 0, w_j = wc, bit t of
@@ -746,13 +762,48 @@ __global__ __launch_bounds__(kTB) void k_class_caps(ShardDev S, const int32_t* s
     red_add(S.red + 66, dfc);
 }
 
-/* this rank's load Σ w·src (the share placement) → red[0] */
+/* the loads Σ w·src of this rank's shares (the share placement) → red[s];
+ * a block's jobs lie in at most two shares (Ps ≥ kTB whenever nsub > 1) */
 __global__ __launch_bounds__(kTB) void k_load(ShardDev S, const int32_t* src) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     long long v = 0;
     if (i < S.NL) v = (long long)S.jc[i].w * src[i];
-    red_add(S.red, v);
+    const int s0 = S.nsub > 1 ? (int)(((int64_t)blockIdx.x * kTB) / S.Ps) : 0;
+    const int sh = (S.nsub > 1 && i < S.NL) ? (int)(i / S.Ps) : s0;
+    red_add(S.red + s0, sh == s0 ? v : 0);
+    if (S.nsub > 1) red_add(S.red + s0 + 1, sh != s0 ? v : 0);
     pub_tail(S);
+}
+
+/* Every share's capacity of every round (sw_share_caps, restated): loads[V]
+ * are the shares' loads in share order (gathered), this rank's shares are
+ * rank·nsub … rank·nsub + nsub − 1.  caps[s·64 + t]; caps[SW_VSHARES·64] = 1
+ * when the shares exist (0 < L ≤ G·T), else 0.  One wave; exact 64-bit
+ * integers (G·T < 2^31, so S·L_r < 2^62; above that no shares). */
+__global__ __launch_bounds__(64) void k_share_caps(const long long* loads, int V, int rank, int nsub, int T,
+                                                   long long G, int32_t* caps) {
+    const int lane = lane_id();
+    long long L = 0;
+    for (int r = 0; r < V; ++r) L += loads[r];
+    const long long C = G * (long long)T;
+    const bool ok = L > 0 && L <= C && T >= 1 && C < (1ll << 31);
+    if (lane == 0) caps[SW_VSHARES * 64] = ok ? 1 : 0;
+    if (!ok) return;
+    const long long Sl = C - L;
+    long long given = 0;
+    for (int r = 0; r < V; ++r) given += Sl * loads[r] / L;
+    const long long rest = Sl - given;
+    long long cursor = 0;
+    for (int r = 0; r < V; ++r) {
+        const long long B = loads[r] + Sl * loads[r] / L + (r < rest ? 1 : 0);
+        const int s = r - rank * nsub;
+        if (s >= 0 && s < nsub && lane < T) {
+            const long long base = B / T, ext = B % T;
+            const long long d = ((long long)lane - cursor + T) % T;
+            caps[s * 64 + lane] = (int32_t)(base + (d < ext ? 1 : 0));
+        }
+        cursor = (cursor + B % T) % T;
+    }
 }
 
 __global__ __launch_bounds__(kTB) void k_copy_words(uint32_t* dst, const uint32_t* src, int64_t n) {
@@ -849,9 +900,11 @@ __global__ __launch_bounds__(kSortThreads) void k_pack_chunk_sort(const sw_pack_
  * threads fill (15 µs per C4 sort; 23 µs with the searches interleaved); the
  * (entry, chunk) grid spreads them over the chip. */
 constexpr int kMergeG = 64; /* lanes per entry, a wave (more chunks: lane q searches q, q + 64, …) */
+/* cpg > 0: the chunks form groups of cpg (the share placement's shares),
+ * each ranked on its own into order[its first entry …] */
 __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, const int32_t* sidx,
                                                          int nchunks, int32_t* order,
-                                                         const int32_t* nact = nullptr) {
+                                                         const int32_t* nact = nullptr, int cpg = 0) {
     const int64_t g = (int64_t)blockIdx.x * kTB + threadIdx.x;
     if (nact) nchunks = (int)((*nact + kSortChunk - 1) / kSortChunk);
     const int64_t s = g / kMergeG; /* groups of kMergeG lanes lie inside one wave */
@@ -861,9 +914,10 @@ __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, cons
     v.h = 0; v.l = 0;
     if (live) v = skeys[s];
     const int c = (int)(s / kSortChunk);
+    const int c0 = cpg > 0 ? c - c % cpg : 0, c1 = cpg > 0 ? c0 + cpg : nchunks;
     int64_t cnt = 0;
     if (live && (v.h | v.l) != 0)
-        for (int qq = q; qq < nchunks; qq += kMergeG) { /* chunks q, q + kMergeG, … */
+        for (int qq = c0 + q; qq < c1; qq += kMergeG) { /* the group's chunks q, q + kMergeG, … */
             if (qq == c) continue;
             const key2* ck = skeys + (int64_t)qq * kSortChunk;
             int pos = 0;
@@ -878,7 +932,7 @@ __global__ __launch_bounds__(kTB) void k_pack_merge_rank(const key2* skeys, cons
 #pragma unroll
     for (int o = kMergeG / 2; o > 0; o >>= 1) pos += __shfl_xor(pos, o, 64);
     if (!live || q != 0 || (v.h == 0 && v.l == 0)) return; /* inactive or padding */
-    order[s - (int64_t)c * kSortChunk + pos] = sidx[s];
+    order[(int64_t)c0 * kSortChunk + s - (int64_t)c * kSortChunk + pos] = sidx[s];
 }
 
 /* the round loop over the global order; writes this rank's rows */
@@ -933,7 +987,8 @@ template <int E, int NT>
 __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_ent* all,
                                                     int64_t M, const int32_t* order,
                                                     uint64_t* ydst, int32_t* pdst,
-                                                    CapsArg caps, int alo, int zero) {
+                                                    CapsArg caps, int alo, int zero,
+                                                    const int32_t* capsd = nullptr) {
     __shared__ sw_xchg_t<NT / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
@@ -941,14 +996,16 @@ __global__ __launch_bounds__(NT) void k_pack_rounds(ShardDev S, const sw_pack_en
     blk.X = &X;
     blk.par = 0;
     const int tid = threadIdx.x;
-    if (caps.has && tid < S.T) capsL[tid] = caps.v[tid];
+    const bool has = caps.has || capsd; /* capsd: one share, workgroup 0 (k_pack_rounds_wave) */
+    if (has && tid < S.T) capsL[tid] = capsd ? capsd[tid] : caps.v[tid];
+    if (capsd && capsd[SW_VSHARES * 64] == 0) return; /* no shares: the wave variant cleared the rows */
     int act = 0;
     for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
     if (A <= alo || A > E * NT) return; /* the other variant places these */
     if (zero) /* a whole placement (not one width class): every row of this rank */
         for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
-    pack_rounds_body<E>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    pack_rounds_body<E>(S, all, A, order, ydst, pdst, has, blk, &PL, capsL);
 }
 
 /* The same round loop on ONE wave (sw_pack_rounds_wave, sw_pack.h): E1
@@ -988,23 +1045,46 @@ __device__ __forceinline__ void pack_rounds_wave_body(const ShardDev& S, const s
 
 /* amax: the largest active count this kernel places (≤ 64·kWaveE); the block
  * variants (k_pack_rounds, alo = amax) place larger ones */
+/* The share placement's form (capsd != nullptr, one workgroup per share):
+ * workgroup b places share b — entries [b·M, b·M + M), its order at b·M, its
+ * capacities capsd[b·64 …] (all rows of the share cleared when the shares do
+ * not exist, capsd[SW_VSHARES·64] = 0) — and clears only the share's rows. */
+__device__ __forceinline__ void share_rows(const ShardDev& S, const int32_t* capsd, int zero, int& r0, int& r1) {
+    r0 = 0;
+    r1 = zero ? S.NL : 0;
+    if (capsd) {
+        r0 = (int)min((int64_t)S.NL, (int64_t)blockIdx.x * S.Ps);
+        r1 = (int)min((int64_t)S.NL, (int64_t)(blockIdx.x + 1) * S.Ps);
+    }
+}
+
 __global__ __launch_bounds__(64) void k_pack_rounds_wave(ShardDev S, const sw_pack_ent* all, int64_t M,
                                                          const int32_t* order, uint64_t* ydst, int32_t* pdst,
-                                                         CapsArg caps, int amax, int zero) {
+                                                         CapsArg caps, int amax, int zero,
+                                                         const int32_t* capsd = nullptr) {
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
     __shared__ uint64_t xmk[64 * kWaveE];
     const int lane = lane_id();
-    if (caps.has && lane < S.T) capsL[lane] = caps.v[lane];
+    const int64_t eb = (int64_t)blockIdx.x * M; /* this workgroup's entries and order */
+    order += eb;
+    const bool has = caps.has || capsd;
+    if (has && lane < S.T) capsL[lane] = capsd ? capsd[blockIdx.x * 64 + lane] : caps.v[lane];
+    int r0, r1;
+    share_rows(S, capsd, zero, r0, r1);
+    if (capsd && capsd[SW_VSHARES * 64] == 0) { /* no shares: nothing placed */
+        for (int i = r0 + lane; i < r1; i += 64) { ydst[i] = 0; pdst[i] = 0; }
+        return;
+    }
     int act = 0;
-    for (int64_t e = lane; e < M; e += 64) act += all[e].st != 0;
+    for (int64_t e = lane; e < M; e += 64) act += all[eb + e].st != 0;
     const int A = wave_sum_i32(act);
     if (A > amax) return; /* the block variant places these */
-    if (zero) /* a whole placement (not one width class): every row of this rank */
-        for (int i = lane; i < S.NL; i += 64) { ydst[i] = 0; pdst[i] = 0; }
+    /* a whole placement (not one width class): every row of this rank, or of the share */
+    for (int i = r0 + lane; i < r1; i += 64) { ydst[i] = 0; pdst[i] = 0; }
     __threadfence_block(); /* the zero rows land before the placed rows below */
     wave_sync();           /* capsL */
-    const int32_t* cl = caps.has ? capsL : nullptr;
+    const int32_t* cl = has ? capsL : nullptr;
     if (A <= 64 * 8) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
     else if (A <= 64 * 16) pack_rounds_wave_body<16>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
     else if (A <= 64 * 32) pack_rounds_wave_body<32>(S, all, A, order, ydst, pdst, cl, &PL, xmk);
@@ -1038,7 +1118,8 @@ int wave_pack_max() {
 template <int NT, int EB>
 __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pack_ent* all, int64_t M,
                                                         const int32_t* order, uint64_t* ydst, int32_t* pdst,
-                                                        CapsArg caps, int alo, int zero) {
+                                                        CapsArg caps, int alo, int zero,
+                                                        const int32_t* capsd = nullptr) {
     __shared__ sw_xchg_t<NT / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
@@ -1046,19 +1127,68 @@ __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pac
     blk.X = &X;
     blk.par = 0;
     const int tid = threadIdx.x;
-    if (caps.has && tid < S.T) capsL[tid] = caps.v[tid];
+    const int64_t eb = (int64_t)blockIdx.x * M; /* this workgroup's entries and order (k_pack_rounds_wave) */
+    order += eb;
+    const bool has = caps.has || capsd;
+    if (has && tid < S.T) capsL[tid] = capsd ? capsd[blockIdx.x * 64 + tid] : caps.v[tid];
+    if (capsd && capsd[SW_VSHARES * 64] == 0) { /* no shares: nothing placed */
+        int r0, r1;
+        share_rows(S, capsd, zero, r0, r1);
+        for (int i = r0 + tid; i < r1; i += NT) { ydst[i] = 0; pdst[i] = 0; }
+        return;
+    }
     int act = 0;
-    for (int64_t e = tid; e < M; e += NT) act += all[e].st != 0;
+    for (int64_t e = tid; e < M; e += NT) act += all[eb + e].st != 0;
     const int A = blk.sum32(act); /* its barrier publishes capsL */
     if (A <= alo || A > (EB > 8 ? EB : 8) * NT) return; /* another variant places these */
-    if (zero) /* a whole placement (not one width class): every row of this rank */
-        for (int i = tid; i < S.NL; i += NT) { ydst[i] = 0; pdst[i] = 0; }
-    if (A <= 2 * NT) pack_rounds_body<2>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
-    else if (A <= 4 * NT) pack_rounds_body<4>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+    int r0, r1;
+    share_rows(S, capsd, zero, r0, r1);
+    /* a whole placement (not one width class): every row of this rank, or of the share */
+    for (int i = r0 + tid; i < r1; i += NT) { ydst[i] = 0; pdst[i] = 0; }
+    if (A <= 2 * NT) pack_rounds_body<2>(S, all, A, order, ydst, pdst, has, blk, &PL, capsL);
+    else if (A <= 4 * NT) pack_rounds_body<4>(S, all, A, order, ydst, pdst, has, blk, &PL, capsL);
     else if (EB <= 8 || A <= 8 * NT)
-        pack_rounds_body<8>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+        pack_rounds_body<8>(S, all, A, order, ydst, pdst, has, blk, &PL, capsL);
     else
-        pack_rounds_body<(EB > 8 ? EB : 8)>(S, all, A, order, ydst, pdst, caps.has != 0, blk, &PL, capsL);
+        pack_rounds_body<(EB > 8 ? EB : 8)>(S, all, A, order, ydst, pdst, has, blk, &PL, capsL);
+}
+
+/* The share placement's round loops in ONE launch (capsd: the shares'
+ * capacities, k_share_caps): workgroup b places share b — entries
+ * [b·M, b·M + M), its order at b·M — on its one-wave loop when the share has
+ * at most wa active entries (wave 0 alone, sw_pack_rounds_wave), else on the
+ * block loop with E = 2, 4 or 8 positions per thread.  One launch for both
+ * forms: as two launches (k_pack_rounds_wave, then k_pack_rounds_sel for the
+ * shares above wa) the C4 placement paid both kernels' ~68 µs in turn
+ * (profiles/r8c4a_*). */
+__global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds_share(ShardDev S, const sw_pack_ent* all, int64_t M,
+                                                                const int32_t* order, uint64_t* ydst,
+                                                                int32_t* pdst, const int32_t* capsd, int wa) {
+    __shared__ sw_xchg_t<SW_BLOCK / 64> X;
+    __shared__ sw_pack_lds PL;
+    __shared__ int32_t capsL[64];
+    __shared__ uint64_t xmk[64 * 8];
+    sw_blk_t<SW_BLOCK / 64> blk;
+    blk.X = &X;
+    blk.par = 0;
+    const int tid = threadIdx.x;
+    const int64_t eb = (int64_t)blockIdx.x * M;
+    order += eb;
+    if (tid < S.T) capsL[tid] = capsd[blockIdx.x * 64 + tid];
+    int r0, r1;
+    share_rows(S, capsd, 1, r0, r1);
+    for (int i = r0 + tid; i < r1; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
+    if (capsd[SW_VSHARES * 64] == 0) return; /* no shares: nothing placed */
+    int act = 0;
+    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[eb + e].st != 0;
+    const int A = blk.sum32(act); /* its barrier publishes capsL and orders the cleared rows first */
+    if (A <= wa && A <= 64 * 8) {
+        if (wave_id() == 0) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, capsL, &PL, xmk);
+        return;
+    }
+    if (A <= 2 * SW_BLOCK) pack_rounds_body<2>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+    else if (A <= 4 * SW_BLOCK) pack_rounds_body<4>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+    else if (A <= 8 * SW_BLOCK) pack_rounds_body<8>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
 }
 
 /* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
@@ -1703,8 +1833,7 @@ struct sw_shard_state {
     bool zero_pending = false;
     /* pinned staging */
     HostBuf<uint8_t> hx;
-    int32_t scaps[SW_TMAX]; /* this rank's share of every round (op_pack_share) */
-    bool share = false;
+    DevBuf<int32_t> scapsd; /* every share's capacities of every round + the shares flag (k_share_caps) */
     std::vector<int32_t> w_all;
     std::vector<uint8_t> hgather;
 };
@@ -2214,19 +2343,27 @@ int op_copy_y(void* ctx, int32_t dst, int32_t src) {
 
 /* local: the share placement — only this rank's entries, no gather, caps is
  * this rank's share of every round (mode 4) or its class capacities (mode 5) */
+/* local: this rank's entries only (no gather) — the share placement (shares:
+ * its shares' device capacities, k_share_caps; one workgroup per share) or a
+ * class-wise repack inside a share (jobs [jlo, jhi), caps = the class's
+ * capacities) */
 int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
-             int32_t wc, const int32_t* caps, bool local = false) {
+             int32_t wc, const int32_t* caps, bool local = false, const int32_t* shares = nullptr,
+             int32_t jlo = 0, int32_t jhi = 0x7FFFFFFF) {
     hipStream_t st = S->h->stream;
-    const int64_t M = local ? S->P : S->P * S->world;
+    const int nsub = shares ? S->dv.nsub : 1;
+    const int64_t Mg = shares ? S->dv.Pp : (local ? S->P : S->P * S->world); /* entries per workgroup */
+    const int64_t M = Mg * nsub;
     CapsArg capsd;
     memset(&capsd, 0, sizeof(capsd));
     if (caps) {
         memcpy(capsd.v, caps, (size_t)S->T * 4);
         capsd.has = 1;
     }
-    LAUNCH(S, k_pack_keys, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
-           (int)wc, S->pall.p + (size_t)S->rank * S->P);
-    const void* gv = S->pall.p + (size_t)S->rank * S->P;
+    sw_pack_ent* mine = shares ? S->pall.p : S->pall.p + (size_t)S->rank * S->P;
+    LAUNCH(S, k_pack_keys, dim3(nblk(shares ? M : S->P)), dim3(kTB), 0, st, S->dv, (int)mode, S->arr[src].p, Mb,
+           (int)wc, mine, shares ? 1 : 0, (int)jlo, (int)jhi);
+    const void* gv = mine;
     if (!local) /* in-place all-gather: the keys go straight to this rank's block */
         SH_TRY(coll_gather(S, S->pall.p + (size_t)S->rank * S->P, S->pall.p,
                            (size_t)S->P * sizeof(sw_pack_ent), nullptr, &gv));
@@ -2235,10 +2372,42 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
     LAUNCH(S, k_pack_chunk_sort, dim3(nch), dim3(kSortThreads), 0, st, all, M, S->skeys.p,
            S->sidx.p);
     LAUNCH(S, k_pack_merge_rank, dim3(nblk((int64_t)nch * kSortChunk * kMergeG)), dim3(kTB), 0, st, S->skeys.p,
-           S->sidx.p, nch, S->porder.p);
+           S->sidx.p, nch, S->porder.p, (const int32_t*)nullptr, nsub > 1 ? (int)(Mg / kSortChunk) : 0);
     const ShardDev dv = S->dv;
     uint64_t* yd = S->y[ydst].p;
     int32_t* pd = S->arr[pdst].p;
+    if (shares) { /* one workgroup per share: the one-wave loop, then the block loop for larger shares */
+        const int wa = wave_pack_max();
+        if (Mg > (nsub > 1 ? 20 : 64) * SW_BLOCK)
+            return S->h->err = "share placement: a share holds more jobs than one workgroup's round loop",
+                   SW_ERR_CAPACITY;
+        if (Mg <= 8 * SW_BLOCK) { /* both loop forms in one launch */
+            LAUNCH(S, k_pack_rounds_share, dim3(nsub), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p, yd, pd,
+                   shares, wa);
+            return SW_OK;
+        }
+        LAUNCH(S, k_pack_rounds_wave, dim3(nsub), dim3(64), 0, st, dv, all, Mg, S->porder.p, yd, pd, capsd, wa, 1,
+               shares);
+        if (Mg > wa) {
+            if (Mg <= 8 * SW_BLOCK) {
+                LAUNCH(S, (k_pack_rounds_sel<SW_BLOCK, 0>), dim3(nsub), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p,
+                       yd, pd, capsd, wa, 1, shares);
+            } else if (Mg <= 20 * SW_BLOCK) {
+                LAUNCH(S, (k_pack_rounds_sel<SW_BLOCK, 20>), dim3(nsub), dim3(SW_BLOCK), 0, st, dv, all, Mg,
+                       S->porder.p, yd, pd, capsd, wa, 1, shares);
+            } else { /* one share (nsub = 1) above 20·512 entries: the wide variants */
+                LAUNCH(S, (k_pack_rounds_sel<SW_BLOCK, 0>), dim3(1), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p,
+                       yd, pd, capsd, wa, 1, shares);
+                if (Mg > 32 * SW_BLOCK)
+                    LAUNCH(S, (k_pack_rounds<64, SW_BLOCK>), dim3(1), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p,
+                           yd, pd, capsd, 8 * SW_BLOCK, 1, shares);
+                else
+                    LAUNCH(S, (k_pack_rounds<32, SW_BLOCK>), dim3(1), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p,
+                           yd, pd, capsd, 8 * SW_BLOCK, 1, shares);
+            }
+        }
+        return SW_OK;
+    }
     /* variants by entries M; above 8 positions per thread also the 8-position
      * variant, for instances whose active jobs fit it (k_pack_rounds) */
 #define SW_LAUNCH_PACK(E, NT, ALO)                                                              \
@@ -2284,70 +2453,70 @@ int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32
     return pack_any((sw_shard_state*)ctx, mode, src, Mb, ydst, pdst, 0, nullptr);
 }
 
-/* twin: e_pack_share (oracle/shard_twin.c) — the ranks' loads all-gathered,
- * this rank's jobs placed alone in its shares (sw_share_caps) */
+/* twin: e_pack_share (oracle/shard_twin.c) — the shares' loads all-gathered,
+ * every share's capacities computed on the device (k_share_caps), this
+ * rank's shares placed side by side, one workgroup each: no host round trip */
 int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     auto* S = (sw_shard_state*)ctx;
-    SH_TRY(zero_red(S, 1));
-    SH_TRY(arm_pub(S, S->dv.red, 8));
-    const bool early = S->dv.pub.dst != nullptr && S->P <= 64 * SW_BLOCK; /* world 1, a placement pack_any runs */
-    LAUNCH(S, k_load, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, S->arr[src].p);
-    disarm_pub(S);
-    if (early) {
-        /* world 1: the share is G in every round whenever there is one
-         * (sw_share_caps), so the placement is enqueued before the host waits
-         * for the load; a load that allows no share placement has its rows
-         * cleared below, after it in stream order */
-        for (int32_t t = 0; t < S->T; ++t) S->scaps[t] = S->dv.G;
-        SH_TRY(pack_any(S, 4, src, 0.0, ydst, pdst, 0, S->scaps, true));
+    hipStream_t st = S->h->stream;
+    const int nsub = S->dv.nsub;
+    SH_TRY(zero_red(S, nsub));
+    LAUNCH(S, k_load, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->arr[src].p);
+    const void* lv = S->dv.red; /* world 1: this rank's loads are every load */
+    if (S->world > 1) {
+        long long* lrecv = reinterpret_cast<long long*>(S->xrecv.p);
+        SH_TRY(coll_gather(S, S->dv.red, lrecv, (size_t)nsub * 8, nullptr, &lv));
     }
-    std::vector<int64_t> loads((size_t)S->world);
-    SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 8, loads.data()));
-    S->share = sw_share_caps(loads.data(), S->world, S->rank, S->T, S->dv.G, S->scaps) == 0;
-    if (!S->share) { /* nothing placed: the gathered orders decide */
-        SH_HIP(S, hipMemsetAsync(S->y[ydst].p, 0, (size_t)S->NL * 8, S->h->stream));
-        SH_HIP(S, hipMemsetAsync(S->arr[pdst].p, 0, (size_t)S->NL * 4, S->h->stream));
-        return SW_OK;
-    }
-    if (early) return SW_OK; /* placed above, with these caps */
-    return pack_any(S, 4, src, 0.0, ydst, pdst, 0, S->scaps, true);
+    LAUNCH(S, k_share_caps, dim3(1), dim3(64), 0, st, (const long long*)lv, nsub * S->world, S->rank, nsub,
+           S->T, (long long)S->dv.G, S->scapsd.p);
+    return pack_any(S, 4, src, 0.0, ydst, pdst, 0, nullptr, true, S->scapsd.p);
 }
 
-/* twin: e_share_repair — this rank's width profile repaired inside its shares
- * (host: sw_profile_repair), every changed class repacked alone (local) */
+/* twin: e_share_repair — each of this rank's shares whose pack stranded
+ * rounds has its width profile repaired inside the share (host:
+ * sw_profile_repair), every changed class repacked alone (local, the share's
+ * jobs only) */
 int op_share_repair(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     auto* S = (sw_shard_state*)ctx;
-    if (!S->share || S->NL <= 0) return SW_OK;
-    const int32_t NL = S->NL, T = S->T;
+    if (S->NL <= 0) return SW_OK;
+    const int32_t NL = S->NL, T = S->T, nsub = S->dv.nsub;
     std::vector<uint64_t> y((size_t)NL);
-    std::vector<int32_t> n((size_t)NL), pl((size_t)NL), w((size_t)NL);
+    std::vector<int32_t> n((size_t)NL), pl((size_t)NL), w((size_t)NL), caps((size_t)SW_VSHARES * 64 + 64);
     hipStream_t st = S->h->stream;
+    SH_HIP(S, hipMemcpyAsync(caps.data(), S->scapsd.p, caps.size() * 4, hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipMemcpyAsync(y.data(), S->y[ydst].p, (size_t)NL * 8, hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipMemcpyAsync(n.data(), S->arr[src].p, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipMemcpyAsync(pl.data(), S->arr[pdst].p, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipMemcpyAsync(w.data(), S->in_w, (size_t)NL * 4, hipMemcpyDeviceToHost, st));
     SH_HIP(S, hipStreamSynchronize(st));
-    int64_t dfc = 0;
-    for (int32_t i = 0; i < NL; ++i) dfc += (int64_t)w[i] * (n[i] - pl[i]);
-    if (dfc == 0) return SW_OK;
-    sw_repair_t R;
-    memset(&R, 0, sizeof(R));
-    for (int32_t i = 0; i < NL; ++i)
-        if (n[i] > 0 && sw_repair_add_class(&R, w[i]) < 0) return SW_OK;
-    for (int32_t t = 0; t < T; ++t) R.L[t] = S->scaps[t];
-    for (int32_t i = 0; i < NL; ++i) {
-        for (int32_t t = 0; t < T; ++t)
-            if ((y[i] >> t) & 1u) R.L[t] -= w[i];
-        if (n[i] <= 0) continue;
-        const int32_t c = sw_repair_class(&R, w[i]);
-        R.M[c] += 1;
-        R.D[c] += n[i] - pl[i];
-        for (int32_t t = 0; t < T; ++t) R.caps[c][t] += (int32_t)((y[i] >> t) & 1u);
-    }
-    if (sw_profile_repair(&R, T) != 0) return SW_OK;
-    for (int32_t c = 0; c < R.ncls; ++c) {
-        if (!R.changed[c]) continue;
-        SH_TRY(pack_any(S, 5, src, 0.0, ydst, pdst, R.wc[c], R.caps[c], true));
+    if (caps[(size_t)SW_VSHARES * 64] == 0) return SW_OK; /* no shares */
+    for (int32_t sh = 0; sh < nsub; ++sh) {
+        const int32_t lo = (int32_t)std::min<int64_t>(NL, sh * S->dv.Ps),
+                      hi = (int32_t)std::min<int64_t>(NL, (sh + 1) * S->dv.Ps);
+        int64_t dfc = 0;
+        for (int32_t i = lo; i < hi; ++i) dfc += (int64_t)w[i] * (n[i] - pl[i]);
+        if (dfc == 0) continue;
+        sw_repair_t R;
+        memset(&R, 0, sizeof(R));
+        bool over = false;
+        for (int32_t i = lo; i < hi && !over; ++i)
+            if (n[i] > 0 && sw_repair_add_class(&R, w[i]) < 0) over = true;
+        if (over) continue;
+        for (int32_t t = 0; t < T; ++t) R.L[t] = caps[(size_t)sh * 64 + t];
+        for (int32_t i = lo; i < hi; ++i) {
+            for (int32_t t = 0; t < T; ++t)
+                if ((y[i] >> t) & 1u) R.L[t] -= w[i];
+            if (n[i] <= 0) continue;
+            const int32_t c = sw_repair_class(&R, w[i]);
+            R.M[c] += 1;
+            R.D[c] += n[i] - pl[i];
+            for (int32_t t = 0; t < T; ++t) R.caps[c][t] += (int32_t)((y[i] >> t) & 1u);
+        }
+        if (sw_profile_repair(&R, T) != 0) continue;
+        for (int32_t c = 0; c < R.ncls; ++c) {
+            if (!R.changed[c]) continue;
+            SH_TRY(pack_any(S, 5, src, 0.0, ydst, pdst, R.wc[c], R.caps[c], true, nullptr, lo, hi));
+        }
     }
     return SW_OK;
 }
@@ -2491,8 +2660,12 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     S->LW = SW_DET_LANES / S->world;
     S->P = S->LW * S->q;
     S->delta = pr->round_duration;
+    const int32_t V = sw_share_count(N, pr->num_gpus, S->world);
+    const int32_t nsub = V / S->world;
+    const int64_t Ps = nsub > 1 ? (int64_t)(SW_DET_LANES / V) * S->q : S->P;
+    const int64_t Pp = nsub > 1 ? (Ps + kSortChunk - 1) / kSortChunk * kSortChunk : S->P;
     const size_t NL = (size_t)std::max<int32_t>(S->NL, 1), T = (size_t)S->T;
-    const size_t M = (size_t)S->P * S->world;
+    const size_t M = std::max<size_t>((size_t)S->P * S->world, (size_t)(nsub * Pp));
     const size_t Mpad = (M + kSortChunk - 1) / kSortChunk * kSortChunk;
     const size_t xbytes = std::max<size_t>({(size_t)(2 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
     bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
@@ -2503,7 +2676,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
                S->porder.reserve(M) || 
-               S->srch.reserve(8) ||
+               S->srch.reserve(8) || S->scapsd.reserve((size_t)SW_VSHARES * 64 + 64) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
@@ -2532,6 +2705,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     v.NL = S->NL; v.T = S->T; v.G = pr->num_gpus; v.nb = pr->num_bases;
     v.LW = (int32_t)S->LW; v.rank = S->rank;
     v.off = off; v.N = N; v.q = S->q; v.P = S->P;
+    v.nsub = nsub; v.Ps = Ps; v.Pp = Pp;
     v.k = pr->regularizer;
     for (int b = 0; b < SW_BMAX; ++b) {
         v.beta[b] = b < pr->num_bases ? pr->bases[b] : 0.0;
@@ -2588,7 +2762,7 @@ void sw_shard_release(sw_handle* h) {
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
     S->p2keys.release();
-    S->srch.release(); S->skeys.release(); S->sidx.release();
+    S->srch.release(); S->skeys.release(); S->sidx.release(); S->scapsd.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;

@@ -182,14 +182,16 @@ static inline int sw_shard_range(int64_t N, int32_t world, int32_t rank, int64_t
  * load, spread like the whole instance's capacity (flat, so its density
  * order front-loads its jobs as the whole instance's would).  At world 1 the
  * share is G in every round: the single-instance pack.  Returns 0, or -1
- * when L = 0 or L > G·T (no share placement).
+ * when L = 0, L > G·T or G·T ≥ 2^31 (no share placement).  "Rank" here is a
+ * share (sw_share_count).
  */
 static inline int sw_share_caps(const int64_t* loads, int32_t W, int32_t rank, int32_t T, int64_t G,
                                 int32_t* caps) {
     __int128 L = 0;
     for (int32_t r = 0; r < W; ++r) L += loads[r];
     const __int128 C = (__int128)G * T;
-    if (L <= 0 || L > C || T < 1) return -1;
+    /* C < 2^31: the engines' 64-bit restatement (k_share_caps) is exact */
+    if (L <= 0 || L > C || T < 1 || C >= ((__int128)1 << 31)) return -1;
     const __int128 S = C - L;
     __int128 given = 0;
     for (int32_t r = 0; r < W; ++r) given += S * loads[r] / L;
@@ -206,6 +208,27 @@ static inline int sw_share_caps(const int64_t* loads, int32_t W, int32_t rank, i
         caps[t] = (int32_t)(base + (d < ext ? 1 : 0));
     }
     return 0;
+}
+
+/*
+ * Shares of the share placement.  A large instance (at least
+ * SW_VSHARE_MIN_JOBS jobs on at least SW_VSHARE_MIN_GPUS GPUs) is placed in
+ * SW_VSHARES lane-aligned shares whatever the world size: share v holds the
+ * jobs sw_shard_range(N, SW_VSHARES, v) and rank r of W (W | SW_VSHARES)
+ * places shares r·S … r·S + S − 1, S = SW_VSHARES / W, one workgroup each.
+ * So the placement — and with it the whole solve — is the same at W = 1, 2,
+ * 4 and 8, and a rank's round loops run side by side on S workgroups instead
+ * of one loop over all its jobs.  Smaller instances, and worlds above
+ * SW_VSHARES, keep one share per rank (at W = 1 the single-instance pack).
+ */
+#define SW_VSHARES 8
+#define SW_VSHARE_MIN_JOBS 4096
+#define SW_VSHARE_MAX_JOBS 65536 /* a share's round loop: at most 20·512 entries */
+#define SW_VSHARE_MIN_GPUS 512
+static inline int32_t sw_share_count(int64_t N, int64_t G, int32_t W) {
+    return (W < SW_VSHARES && N >= SW_VSHARE_MIN_JOBS && N <= SW_VSHARE_MAX_JOBS && G >= SW_VSHARE_MIN_GPUS)
+               ? SW_VSHARES
+               : W;
 }
 
 /* The combining phase of sw_detsum (oracle/plan_twin.c) over the lane partials. */

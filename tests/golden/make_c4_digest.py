@@ -1,10 +1,12 @@
 """Generate tests/golden/c4_digest.json: the CPU solves of the C4 instance that
 bench.py's c4_sharded sub-record solves sharded over N GPUs — the twin
-(oracle/plan_twin.c, the single-instance solve, = the sharded solve at world 1)
-and the CPU shard engine (oracle/shard_twin.c, the specification of the GPU
-shard engine) at worlds 2, 4 and 8, where the share placement makes the plan
-rows depend on the world size.  bench.py checks its gathered
-plan / counts / objective against the digest of its world size.
+(oracle/plan_twin.c, the single-instance solve: top-level digest) and the CPU
+shard engine (oracle/shard_twin.c, the specification of the GPU shard engine)
+at worlds 1, 2, 4 and 8 (by_world).  The C4 instance is placed in
+SW_VSHARES = 8 shares at every world size (sw_share_count), so
+the four sharded digests are one and the same; it shares the single
+instance's counts and P1 objective, not its plan rows.  bench.py checks its
+gathered plan / counts / objective against the digest of its world size.
 
     python tests/golden/make_c4_digest.py
 """
@@ -52,7 +54,8 @@ def main():
                                                                           dtype=sn.np.int32).tobytes()).hexdigest()[:32],
                       "objective_hex": float(r["objective"]).hex(),
                       "p2_objective": float(r["p2_objective"]), "status": int(r["status"])}
-    assert by["1"]["plan_sha"] == out["plan_sha"] and by["1"]["objective_hex"] == out["objective_hex"]
+    assert all(by[w] == by["1"] for w in by), "the sharded C4 solve depends on the world size"
+    assert by["1"]["counts_sha"] == out["counts_sha"] and by["1"]["objective_hex"] == out["objective_hex"]
     out["by_world"] = by
     json.dump(out, open(OUT, "w"), indent=1)
     print(out)

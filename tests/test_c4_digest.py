@@ -1,9 +1,10 @@
 """The committed C4 digests (tests/golden/c4_digest.json) that bench.py's
 c4_sharded sub-record checks at every N are the CPU solves of that instance —
-the twin's at world 1, the CPU shard engine's at worlds 2, 4, 8 (DESIGN.md
-§7.2: the share placement's rows depend on W) — so a stale digest fails here,
-on the CPU, before a GPU run; and on the GPU the RCCL-sharded engine at world
-1 reproduces the world-1 digest."""
+the twin's single-instance solve (top level) and the CPU shard engine's at
+worlds 1, 2, 4, 8 (by_world; DESIGN.md §7.2: the C4 instance is placed in
+SW_VSHARES = 8 shares at every world size, so the four are one digest) — so a
+stale digest fails here, on the CPU, before a GPU run; and on the GPU the
+RCCL-sharded engine at world 1 reproduces the world-1 digest."""
 import hashlib
 import json
 import os
@@ -53,7 +54,13 @@ def test_c4_digest_is_the_twin_solve(twin):
     assert float(r["objective"]).hex() == GOLD["objective_hex"]
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+def test_c4_world_digests_are_one():
+    ref = GOLD["by_world"]["1"]
+    assert all(GOLD["by_world"][w] == ref for w in ("2", "4", "8"))
+    assert ref["counts_sha"] == GOLD["counts_sha"] and ref["objective_hex"] == GOLD["objective_hex"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_c4_world_digests_are_the_shard_engine(world, twin):
     """The CPU shard engine at W (threads) reproduces the committed digest of W,
     and keeps the single-instance P1 objective (the share placement places
@@ -92,6 +99,7 @@ def test_gpu_rccl_world1_reproduces_c4_digest():
     s.dist_init(sn.unique_id(), 0, 1)
     r = s.dist_solve(a, 0, a.N)
     s.close()
-    assert digest(r["plan"], r["planned_rounds"]) == (GOLD["plan_sha"], GOLD["counts_sha"])
-    assert float(r["objective"]).hex() == GOLD["objective_hex"]
+    g = GOLD["by_world"]["1"]
+    assert digest(r["plan"], r["planned_rounds"]) == (g["plan_sha"], g["counts_sha"])
+    assert float(r["objective"]).hex() == g["objective_hex"] == GOLD["objective_hex"]
     check_lp_bound(r["objective"])

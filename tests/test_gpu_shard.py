@@ -17,7 +17,7 @@ import pytest
 import sw_native as sn
 import sw_synth as ss
 from helpers import check_plan_valid
-from test_shard import (CASES, ThreadGroup, assemble, assert_same_as_single, run_threads,  # noqa: F401
+from test_shard import (CASES, ThreadGroup, assemble, assert_same_as_single, assert_share_contract, run_threads,  # noqa: F401
                         shard_lib)
 
 pytestmark = pytest.mark.gpu
@@ -78,13 +78,16 @@ def test_gpu_shard_host_comm(case, world, shard_lib):
     assert_same_as_single(r, run_threads(shard_lib, a, world), f"W={world} {case}")
 
 
-def test_gpu_shard_c4_shape(rccl_solver, twin):
-    """The 10k-job × 30-round C4 instance, whole on one rank."""
+def test_gpu_shard_c4_shape(rccl_solver, twin, shard_lib):
+    """The 10k-job × 30-round C4 instance, whole on one rank:
+    the CPU shard engine at world 1 bit for bit (its eight shares placed by
+    eight workgroups, sw_share_count), and so the result of every world size."""
     c = ss.C4
     a = ss.synth_problem(11, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
     r = rccl_solver.dist_solve(a, 0, a.N)
     check_plan_valid(a, r)
-    assert_same_as_single(r, twin.solve(a), "C4")
+    assert_same_as_single(r, run_threads(shard_lib, a, 1), "C4")
+    assert_share_contract(r, twin.solve(a), "C4 vs single")
 
 
 def test_gpu_shard_c4_world8(shard_lib):

@@ -6,16 +6,20 @@ for the multi-process path, as W=2 processes over torch.distributed gloo.
 
 The contract.  The CPU shard engine is the specification the
 GPU engine (csrc/sw_shard.hip) matches bit for bit at every world size
-(tests/test_gpu_shard.py).  Against the single-instance solve (the twin,
-oracle/plan_twin.c, = the GPU plan kernel):
-  * W = 1: the same result, bit for bit (plan rows, counts, every objective);
-  * W > 1: every rank places its own jobs in its share of each round (the
-    share placement, sw_share_caps), so the plan rows and the P2 objective
-    depend on W; P1 — counts, objective, utility, makespan, bound and the P1
-    status bits — is the single-instance solve's bit for bit (the same level
-    search, every count placed), or better when only the shares could place
-    the level search's counts; P2 stays within SHARE_P2_RATIO of the single
-    instance's.  Only `iters` differs at every W (it counts collective steps).
+(tests/test_gpu_shard.py).  The placement runs in V = sw_share_count(N, G, W)
+shares (each placed alone in its share of every round, sw_share_caps): V = W,
+except for large instances (≥ 4,096 jobs on ≥ 512 GPUs), which take V = 8 at
+every W ≤ 8.  Against the single-instance solve (the twin, oracle/plan_twin.c,
+= the GPU plan kernel):
+  * V = 1 (W = 1, not large): the same result, bit for bit (plan rows, counts,
+    every objective);
+  * V > 1: the plan rows and the P2 objective depend on V (not on W: a large
+    instance gives the same result at W = 1, 2, 4, 8); P1 — counts,
+    objective, utility, makespan, bound and the P1 status bits — is the
+    single-instance solve's bit for bit (the same level search, every count
+    placed), or better when only the shares could place the level search's
+    counts; P2 stays within SHARE_P2_RATIO of the single instance's.  Only
+    `iters` differs at every W (it counts collective steps).
 """
 import ctypes
 import os
@@ -131,8 +135,13 @@ def assert_share_contract(rs, rt, what):
         assert rs["objective"] >= rt["objective"], what
 
 
-def assert_contract(rs, rt, world, what):
-    if world == 1:
+def share_count(N, G, world):
+    """sw_share_count (csrc/sw_shard_ctl.h)."""
+    return 8 if world < 8 and 4096 <= N <= 65536 and G >= 512 else world
+
+
+def assert_contract(rs, rt, world, what, N=0, G=0):
+    if share_count(N, G, world) == 1:
         assert_same_as_single(rs, rt, what)
     else:
         assert_share_contract(rs, rt, what)
@@ -171,7 +180,7 @@ def test_sharded_vs_single(case, world, shard_lib, twin):
     rs = run_threads(shard_lib, a, world)
     rt = twin.solve(a)
     check_plan_valid(a, rs)
-    assert_contract(rs, rt, world, f"W={world} case {case}")
+    assert_contract(rs, rt, world, f"W={world} case {case}", N, G)
 
 
 def test_sharded_edge_cases(shard_lib, twin):
@@ -274,7 +283,7 @@ def test_sharded_fuzz_vs_single(world, shard_lib, twin):
         a = fuzz_problem(s)
         rs = run_threads(shard_lib, a, world)
         check_plan_valid(a, rs)
-        assert_contract(rs, twin.solve(a), world, f"W={world} fuzz seed {s}")
+        assert_contract(rs, twin.solve(a), world, f"W={world} fuzz seed {s}", a.N, a.G)
 
 
 @pytest.mark.parametrize("world", [1, 2, 4])
@@ -294,7 +303,7 @@ def test_sharded_pattern_placement_equals_single(world, shard_lib, twin):
         rs = run_threads(shard_lib, a, world)
         check_plan_valid(a, rs)
         rt = twin.solve(a)
-        assert_contract(rs, rt, world, f"W={world} frag seed {s}")
+        assert_contract(rs, rt, world, f"W={world} frag seed {s}", a.N, a.G)
         if s == 50115:
             assert not rt["status"] & sn.SW_STATUS_P1_REPACKED  # placed as counted
 
@@ -373,3 +382,18 @@ def test_share_caps_properties(shard_lib):
             assert (rows[0] == G).all()
     assert caps_of([0, 0], 2, 0, 4, 10)[0] == -1
     assert caps_of([30, 11], 2, 0, 4, 10)[0] == -1
+
+
+def test_large_instance_same_at_every_world(shard_lib, twin):
+    """A large instance (5,000 jobs on 1,424 GPUs: V = 8 shares at every
+    W ≤ 8) gives one result at W = 1, 2, 4, 8 — plan rows, counts and every
+    objective bit for bit; at W = 16 (V = W) the shares are its own."""
+    a = ss.synth_problem(11, 5000, 1424, 30, 120.0, 1e5, 5.0)
+    r1 = run_threads(shard_lib, a, 1)
+    check_plan_valid(a, r1)
+    assert_share_contract(r1, twin.solve(a), "W=1 large")
+    for world in (2, 4, 8):
+        assert_same_as_single(run_threads(shard_lib, a, world), r1, f"W={world} vs W=1")
+    r16 = run_threads(shard_lib, a, 16)
+    check_plan_valid(a, r16)
+    assert_share_contract(r16, twin.solve(a), "W=16 large")
