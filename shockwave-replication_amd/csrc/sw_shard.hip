@@ -127,6 +127,18 @@ struct ShardDev {
     } pub;
 };
 
+/* Device-side state of a solve's common path (fast_solve): every decision the
+ * controller (sw_shard_ctl.h) makes on that path, taken by the kernels from
+ * the step results in device memory instead of by the host.  escape != 0:
+ * the solve left the common path (a width tail, a level search that needs
+ * its branch and bound, a share pack that strands rounds, invalid inputs);
+ * the host then solves it again with the host-driven controller. */
+struct FastCtl {
+    long long C, bud, Wall, wt, rem, used;
+    int all, escape, did_between, pad;
+    double k, A, M_lo, U, Mact, ubound, Umax, bmax;
+};
+
 struct Thresholds {
     uint64_t v[SW_SHARD_K]; /* u32 key bits or fp64 bits, ascending */
     int32_t K;
@@ -260,7 +272,10 @@ __global__ __launch_bounds__(kTB) void k_keys(ShardDev S) {
 
 /* ---- SELECT steps ----------------------------------------------------------- */
 
-__global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf) {
+/* Mdev (fast_solve): M = the level search's answer, its state's lo bits */
+__global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf,
+                                               const unsigned long long* Mdev = nullptr) {
+    if (Mdev) M = sw_from_bits(Mdev[0]);
     const int i = blockIdx.x * kTB + threadIdx.x;
     long long wf = 0, wall = 0;
     if (i < S.NL) {
@@ -445,10 +460,18 @@ __global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, co
     }
 }
 
-__global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b) {
+/* c (fast_solve): the interval (M_lo, M_lo + wmax] of FastCtl, nothing to
+ * count when wmax ≤ 0 */
+__global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b, const FastCtl* c = nullptr) {
     const int i = blockIdx.x * kTB + threadIdx.x;
     long long cnt = 0;
-    if (i < S.NL) {
+    bool run = true;
+    if (c) {
+        a = c->M_lo;
+        b = c->bmax;
+        run = c->did_between != 0;
+    }
+    if (run && i < S.NL) {
         const sw_jobc c = S.jc[i];
         const int n1 = tj_of(S, c) + 1;
         const int d = g_count_gt(c, n1, a) - g_count_ge(c, n1, b);
@@ -466,18 +489,24 @@ __global__ __launch_bounds__(kTB) void k_take_all(ShardDev S) {
     S.taken[i] = tj - S.l[i];
 }
 
-__global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
+/* rdev / fc (fast_solve): ρ = the price search's answer; when every item
+ * fits (fc->all) the step is k_take_all's (n := T_j, taken := T_j − l) */
+__global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho, const unsigned long long* rdev = nullptr,
+                                              const FastCtl* fc = nullptr) {
     const int i = blockIdx.x * kTB + threadIdx.x;
+    if (rdev) rho = (uint32_t)rdev[0];
+    const bool all = fc && fc->all;
     long long wt = 0, tie = 0;
     if (i < S.NL) {
         const sw_jobc c = S.jc[i];
         const int tj = tj_of(S, c), l = S.l[i];
         const float* row = S.keys + (size_t)i * S.T;
-        const int tk = key_count<false>(row, l, tj, rho);
+        const int tk = all ? tj - l : key_count<false>(row, l, tj, rho);
         S.taken[i] = tk;
         wt = (long long)c.w * tk;
-        tie = (long long)c.w * (key_count<true>(row, l, tj, rho) - tk);
+        tie = all ? 0 : (long long)c.w * (key_count<true>(row, l, tj, rho) - tk);
         S.tie[i] = (int32_t)tie;
+        if (all) S.arr[SW_A_N][i] = tj;
     }
     red_add(S.red + 0, wt);
     red_add(S.red + 1, tie);
@@ -499,7 +528,26 @@ __global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho) {
  * k_take summed for blocks 0 … b−1, then a block scan: the same integer
  * prefix as a walk over the jobs in order, without one workgroup walking
  * them all. */
-__global__ __launch_bounds__(kTB) void k_assign(ShardDev S, long long rem, long long excl0) {
+/* fc / g (fast_solve): rem = bud − Σ_ranks wt and excl0 = Σ of the tie
+ * weights of the ranks before this one, from k_take's gathered results g
+ * (2 per rank); nothing to assign when every item fits */
+__global__ __launch_bounds__(kTB) void k_assign(ShardDev S, long long rem, long long excl0,
+                                                FastCtl* fc = nullptr, const long long* g = nullptr,
+                                                int world = 1) {
+    if (fc) {
+        if (fc->all) return; /* used = 0 (the zeroed step slot) */
+        long long wt = 0, ex = 0;
+        for (int r = 0; r < world; ++r) {
+            wt += g[2 * r];
+            if (r < S.rank) ex += g[2 * r + 1];
+        }
+        rem = fc->bud - wt;
+        excl0 = ex;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            fc->wt = wt;
+            fc->rem = rem;
+        }
+    }
     __shared__ long long ws[kTB / 64];
     __shared__ long long boff;
     long long pb = 0;
@@ -687,6 +735,167 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
         __syncthreads();
         pub_store(S);
     }
+}
+
+/* ---- device-side control of the common path (fast_solve) -------------------------
+ * One-wave kernels between the step kernels: each takes the controller's
+ * decisions (sw_shard_ctl.h) from the step results in device memory, so the
+ * host enqueues the whole solve and reads one result. */
+
+/* sw_shard_tree on one wave: lane l holds lane 64·w + l of chunk w (lane
+ * partial ℓ of the gathered eval blocks: rank ℓ / LW, offset ℓ mod LW), each
+ * chunk halved by shuffles (p[i] + p[i + h], the same operands as the host
+ * loop), then the eight chunk sums by the same halving.  Wave-uniform result. */
+__device__ __forceinline__ double wave_tree512(const double* blocks, int blk, int LW, int part) {
+    const int lane = lane_id();
+    double ws[SW_DET_LANES / 64];
+#pragma unroll
+    for (int w = 0; w < SW_DET_LANES / 64; ++w) {
+        const int idx = 64 * w + lane, r = idx / LW, o = idx - r * LW;
+        double v = blocks[(size_t)r * blk + (size_t)part * LW + o];
+#pragma unroll
+        for (int h = 32; h >= 1; h >>= 1) v = v + __shfl_down(v, h, 64);
+        ws[w] = __shfl(v, 0, 64);
+    }
+#pragma unroll
+    for (int h = SW_DET_LANES / 128; h >= 1; h >>= 1)
+#pragma unroll
+        for (int i = 0; i < h; ++i) ws[i] = ws[i] + ws[i + h];
+    return ws[0];
+}
+
+/* max g and Σ isum over the gathered eval blocks (op_eval's host loop) */
+__device__ __forceinline__ void blocks_gm_isum(const double* blocks, int blk, int LW, int W, double& gm,
+                                               long long& is) {
+    gm = 0.0;
+    is = 0;
+    for (int r = 0; r < W; ++r) {
+        const double* b = blocks + (size_t)r * blk;
+        gm = sw_max(gm, b[2 * LW]);
+        is += reinterpret_cast<const long long*>(b)[2 * LW + 1];
+    }
+}
+
+/* after setup: the level search's bracket [lb, top) and budget C */
+__global__ void k_fast_lvl_init(FastCtl* c, const long long* R0, unsigned long long* sr, long long C, double k) {
+    if (threadIdx.x != 0) return;
+    FastCtl z;
+    memset(&z, 0, sizeof(z));
+    z.C = C;
+    z.k = k;
+    z.A = sw_from_bits((uint64_t)R0[0]);
+    z.escape = R0[2] != 0; /* invalid inputs: the host path reports them */
+    *c = z;
+    sr[0] = (unsigned long long)R0[1];
+    sr[1] = (unsigned long long)R0[3];
+    sr[2] = (unsigned long long)C;
+    sr[3] = 0;
+}
+
+/* after the forcing step at M_lo (swc_select): budget, every item fits or
+ * the price search's bracket [0, SW_KEY_INF_BITS) */
+__global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigned long long* srl,
+                                  unsigned long long* sp) {
+    if (threadIdx.x != 0) return;
+    const long long Wf = R1[0], Wall = R1[1];
+    c->M_lo = sw_from_bits(srl[0]);
+    if (Wf > c->C) c->escape = 1; /* not at M_lo: a guard */
+    const long long bud = c->C - Wf;
+    const int all = Wall <= bud || Wf > c->C;
+    c->bud = bud;
+    c->Wall = Wall;
+    c->all = all;
+    sp[0] = 0;
+    sp[1] = all ? 0ull : (unsigned long long)SW_KEY_INF_BITS;
+    sp[2] = (unsigned long long)bud;
+    sp[3] = 0;
+}
+
+/* after the SELECT and UMAX evaluations: U, max g, the Lagrangian bound, the
+ * utility optimum and the interval the level search counts next
+ * (swc_select / swc_level_search); a width tail leaves the common path */
+/* Every gathered view is consumed by the kernel right after its gather (the
+ * peer transport's region half is rewritten two exchanges later). */
+__global__ __launch_bounds__(64) void k_fast_sel_sum(FastCtl* c, const double* sel, int W, int LW) {
+    const int blk = 2 * LW + 2;
+    const double U = wave_tree512(sel, blk, LW, 0);
+    const double Bt = wave_tree512(sel, blk, LW, 1);
+    if (lane_id() != 0) return;
+    double gm;
+    long long is;
+    blocks_gm_isum(sel, blk, LW, W, gm, is);
+    c->U = U;
+    c->Mact = gm;
+    c->Umax = Bt; /* the B tree, until k_fast_sel_ctl */
+}
+
+__global__ __launch_bounds__(64) void k_fast_sel_ctl(FastCtl* c, const long long* R3, const double* umax,
+                                                     const unsigned long long* sp, int W, int LW) {
+    const int blk = 2 * LW + 2;
+    const double Um = wave_tree512(umax, blk, LW, 0);
+    if (lane_id() != 0) return;
+    (void)W;
+    const int all = c->all;
+    if (!all && c->rem - R3[0] > 0) c->escape = 1; /* the width tail: host path */
+    const double rho_d = all ? 0.0 : (double)sw_float_of((uint32_t)sp[0]);
+    const long long wgt = all ? c->Wall : c->wt;
+    const double U = c->U, Bt = c->Umax;
+    c->ubound = Bt + (rho_d * c->A) * (double)(c->bud - wgt);
+    c->Umax = Um;
+    const double wmax = (Um - U) / c->k;
+    c->did_between = wmax > 0.0;
+    c->bmax = c->M_lo + wmax;
+}
+
+/* after the PACKED evaluation: rounds the share placement stranded */
+__global__ __launch_bounds__(64) void k_fast_packed(FastCtl* c, const double* packed, int W, int LW) {
+    if (lane_id() != 0) return;
+    double gp;
+    long long dfc;
+    blocks_gm_isum(packed, 2 * LW + 2, LW, W, gp, dfc);
+    if (dfc != 0) c->escape = 1; /* the share repair, the gathered orders: host path */
+}
+
+/* the solve's result: P1 from the level search, P2 and the plan from the
+ * final evaluation (sw_shard_solve's common path), to pinned host memory
+ * (words: objective, utility, makespan, p2, bound as f64; iters, status,
+ * escape, transport error as i32), then the flag's release */
+struct FastOut {
+    double objective, utility, makespan, p2, bound;
+    int32_t iters, status, escape, xerr;
+};
+__global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long long* R4,
+                                                   const long long* R5, const double* fin,
+                                                   const unsigned long long* srl, const unsigned long long* sp,
+                                                   int W, int LW, FastOut* hout, unsigned long long* hflag,
+                                                   unsigned long long hseq, const int* xerr) {
+    const int blk = 2 * LW + 2;
+    const double U = wave_tree512(fin, blk, LW, 0);
+    const double P2 = wave_tree512(fin, blk, LW, 1);
+    if (lane_id() != 0) return;
+    double gm;
+    long long any;
+    blocks_gm_isum(fin, blk, LW, W, gm, any);
+    FastOut o;
+    o.escape = c->escape || (c->did_between && R4[0] != 0); /* the branch and bound: host path */
+    o.utility = U;
+    o.p2 = P2;
+    o.makespan = gm;
+    o.objective = U - c->k * gm;
+    o.bound = c->ubound - c->k * c->M_lo;
+    int32_t st = 0;
+    if (R5[0] > 0) st |= SW_STATUS_P2_EXCHANGED;
+    if (any == 0) st |= SW_STATUS_NO_PLANNED;
+    if (sw_p1_uncertified(o.objective, o.bound)) st |= SW_STATUS_P1_UNCERTIFIED;
+    o.status = st;
+    /* setup, level rounds, force, [price rounds, take, assign], SELECT, UMAX,
+     * [between], share pack, PACKED, exchange, FINAL (swc_* step counts) */
+    o.iters = (int32_t)(1 + (long long)srl[3] + 1 + (c->all ? 0 : (long long)sp[3] + 2) + 2 +
+                        (c->did_between ? 1 : 0) + 4);
+    o.xerr = xerr ? *xerr : 0;
+    *hout = o;
+    __threadfence_system();
+    __hip_atomic_store(hflag, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 /* ---- placement ---------------------------------------------------------------- */
@@ -1822,7 +2031,8 @@ struct sw_shard_state {
     DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry), prepared set-up */
     DevBuf<sw_pack_ent> p2keys; /* the exchange's rank-sort keys (k_p2x_pre0) */
     DevBuf<unsigned char> rrin, rrrow, rrws; /* re-optimisation: gathered entries, workspace */
-    DevBuf<unsigned long long> srch; /* device-chained search state (k_search_*) */
+    DevBuf<unsigned long long> srch; /* device-chained search states (k_search_*): level [0, 8), price [8, 16) */
+    DevBuf<FastCtl> fctl;            /* fast_solve's device-side controller state */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
     DevBuf<int32_t> sidx; /* their entries */
     /* this solve's per-job inputs on the device: the buffers above after an
@@ -2165,25 +2375,17 @@ int op_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
  * the worst-case number of rounds enqueued (closed rounds are no-ops), one
  * read-back at the end.  RCCL or a single rank only: host collectives need
  * the host between rounds and use the controller's loop. */
-int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
-              int32_t* rounds) {
-    auto* S = (sw_shard_state*)ctx;
+/* The rounds of a device-chained K-ary search on the state at sb[0..3] (set
+ * in stream order before): nr rounds probe → (collective) → the step applied
+ * in the next round's probe, then the last step in place.  *fin = the final
+ * state (lo = the answer, [3] = the rounds taken).  Searches whose bracket
+ * closes early leave their last rounds empty. */
+int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* sb,
+                   unsigned long long** fin, bool arm = false) {
     hipStream_t st = S->h->stream;
-    /* each round leaves a span ≤ ⌊span / 64⌋, so the rounds are at most the
-     * base-64 digits of the initial span */
-    int nr = 0;
-    for (uint64_t sp = lo < hi ? hi - lo : 0; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nr;
-    *rounds = 0;
-    *out = lo;
-    if (nr == 0) return SW_OK;
-    /* search states X_r alternate between srch[0..3] and srch[4..7]: round r
-     * reads X_{r−1}, applies round r − 1's step and stores X_r (k_probe_dev) */
-    unsigned long long* sb = S->srch.p;
     /* round r reads round r − 1's slice: keep the nr slices inside one pass of
      * the ring (a wrap clears the whole ring) */
     if (S->ring_pos + nr > kRing) S->ring_pos = kRing;
-    LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sb, (unsigned long long)lo,
-           (unsigned long long)hi, (long long)bud);
     const unsigned pb = nblk((int64_t)S->NL * S->T);
     const long long* prev = nullptr;
     for (int r = 0; r < nr; ++r) {
@@ -2198,15 +2400,39 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
             LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev);
         if (S->peer)
             SH_TRY(peer_xchg(S, S->dv.red, (size_t)(SW_SHARD_K + 1) * 8, 0, SW_SHARD_K + 1, S->dv.red));
-        else if (S->comm)
+        else if (S->comm && S->world > 1)
             SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
                                      S->comm, st));
         prev = S->dv.red;
     }
     unsigned long long* sr = sb + 4 * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
-    SH_TRY(arm_pub(S, sr, 32));
+    if (arm) SH_TRY(arm_pub(S, sr, 32)); /* world 1: the update publishes the state itself */
     LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev, S->dv);
     disarm_pub(S);
+    *fin = sr;
+    return SW_OK;
+}
+
+/* swc_search with every round on the stream: probe → (all-reduce) → update,
+ * the worst-case number of rounds enqueued (closed rounds are no-ops), one
+ * read-back at the end.  RCCL or a single rank only: host collectives need
+ * the host between rounds and use the controller's loop. */
+int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
+              int32_t* rounds) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    /* each round leaves a span ≤ ⌊span / 64⌋, so the rounds are at most the
+     * base-64 digits of the initial span */
+    int nr = 0;
+    for (uint64_t sp = lo < hi ? hi - lo : 0; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nr;
+    *rounds = 0;
+    *out = lo;
+    if (nr == 0) return SW_OK;
+    unsigned long long* sb = S->srch.p;
+    LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sb, (unsigned long long)lo,
+           (unsigned long long)hi, (long long)bud);
+    unsigned long long* sr = nullptr;
+    SH_TRY(enqueue_search(S, kind, nr, sb, &sr, true));
     unsigned long long v[4];
     SH_TRY(publish(S, sr, sizeof(v), v));
     *out = v[0];
@@ -2287,9 +2513,11 @@ int op_fill_apply(void* ctx, int64_t jb, int32_t t) {
     return SW_OK;
 }
 
-int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
-            int64_t* isum) {
-    auto* S = (sw_shard_state*)ctx;
+/* A reduction step on the stream: k_eval into this rank's block of the
+ * gather buffer, gathered in rank order (hout: also to the host).  *view =
+ * where the gathered blocks are on the device (the peer transport's region
+ * half: read it before the second exchange after this one). */
+int eval_enqueue(sw_shard_state* S, int32_t sel, int32_t arg, const double** view, double* hout) {
     const int64_t LW = S->LW, blk = 2 * LW + 2;
     SH_TRY(zero_red(S, 2));
     const int32_t* arr = sel == SW_EV_GMAX || sel == SW_EV_PACKED ? S->arr[arg].p : nullptr;
@@ -2298,12 +2526,22 @@ int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB,
     const int lpb = (int)std::max<int64_t>(1, kTB / S->q);
     double* xs = S->xrecv.p + (size_t)S->rank * blk; /* in-place all-gather */
     if (S->q > kTB) return S->h->err = "eval: more than 256 jobs per lane", SW_ERR_CAPACITY;
-    SH_TRY(arm_pub(S, xs, (size_t)blk * 8));
+    if (hout) SH_TRY(arm_pub(S, xs, (size_t)blk * 8));
     LAUNCH(S, k_eval, dim3((unsigned)((LW + lpb - 1) / lpb)), dim3(kTB), 0, S->h->stream, S->dv,
            (int)sel, arr, ys, (int)(arg & 0xFF), (int)(arg >> 8), lpb, xs);
     disarm_pub(S);
+    const void* v = S->xrecv.p;
+    SH_TRY(coll_gather(S, xs, S->xrecv.p, (size_t)blk * 8, hout, &v));
+    if (view) *view = (const double*)v;
+    return SW_OK;
+}
+
+int op_eval(void* ctx, int32_t sel, int32_t arg, double* lanesA, double* lanesB, double* gm,
+            int64_t* isum) {
+    auto* S = (sw_shard_state*)ctx;
+    const int64_t LW = S->LW, blk = 2 * LW + 2;
     std::vector<double> all((size_t)blk * S->world);
-    SH_TRY(coll_gather(S, xs, S->xrecv.p, (size_t)blk * 8, all.data()));
+    SH_TRY(eval_enqueue(S, sel, arg, nullptr, all.data()));
     double g = 0.0;
     int64_t s = 0;
     for (int r = 0; r < S->world; ++r) {
@@ -2545,8 +2783,9 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc
 
 /* twin: e_p2x (oracle/shard_twin.c) — gather the P2 placement, run the
  * exchange step replicated, keep this rank's rows */
-int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
-    auto* S = (sw_shard_state*)ctx;
+/* the exchange step on the stream; *res = the step slot whose [0] receives
+ * the cycles cancelled (the same on every rank); arm: publish it (world 1) */
+int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, bool arm) {
     hipStream_t st = S->h->stream;
     const int64_t M = S->P * S->world;
     if (S->p2ws.reserve((size_t)M * SW_P2X_ARR_BYTES)) return host_fail(S, "P2 exchange workspace");
@@ -2605,10 +2844,18 @@ int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
         pre.Wb = Wb;
         pre.Wk = Wk;
     }
-    SH_TRY(arm_pub(S, S->dv.red, 8));
+    if (arm) SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_p2x, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, (const p2x_ent*)gv, M, S->p2ws.p,
            S->y[ysrc].p, pre, (int)prepared);
     disarm_pub(S);
+    *res = S->dv.red;
+    return SW_OK;
+}
+
+int op_p2x(void* ctx, int32_t ysrc, int32_t nsrc, int32_t* cancels) {
+    auto* S = (sw_shard_state*)ctx;
+    long long* r = nullptr;
+    SH_TRY(p2x_enqueue(S, ysrc, nsrc, &r, true));
     uint64_t nc = 0;
     SH_TRY(coll_reduce(S, S->dv.red, 1, 1, &nc)); /* every rank computed the same count */
     *cancels = (int32_t)nc;
@@ -2676,7 +2923,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
                S->porder.reserve(M) || 
-               S->srch.reserve(8) || S->scapsd.reserve((size_t)SW_VSHARES * 64 + 64) ||
+               S->srch.reserve(16) || S->fctl.reserve(1) || S->scapsd.reserve((size_t)SW_VSHARES * 64 + 64) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
@@ -2762,7 +3009,7 @@ void sw_shard_release(sw_handle* h) {
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
     S->p2keys.release();
-    S->srch.release(); S->skeys.release(); S->sidx.release(); S->scapsd.release();
+    S->srch.release(); S->skeys.release(); S->sidx.release(); S->scapsd.release(); S->fctl.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
@@ -3001,6 +3248,150 @@ int sw_dist_enable_peer(sw_handle* h, int64_t max_total_jobs) {
 }
 
 namespace {
+int slow_solve(sw_shard_state* S, const sw_problem* local, int64_t total_jobs, sw_result* res, bool dirty);
+
+/* An all-reduce of n step words in place, on the stream, without the host
+ * (fast_solve): the identity at world 1, RCCL or the peer transport above. */
+int coll_dev_reduce(sw_shard_state* S, void* dbuf, int n, int op) {
+    if (S->world == 1) return SW_OK;
+    if (S->peer) return peer_xchg(S, dbuf, (size_t)n * 8, op, n, dbuf);
+    if (!S->comm) return S->h->err = "fast path: no device collective", SW_ERR_INVALID;
+    const ncclDataType_t ty = op == 0 ? ncclInt64 : op == 1 ? ncclUint64 : ncclFloat64;
+    SH_NCCL(S, ncclAllReduce(dbuf, dbuf, (size_t)n, ty, op == 0 ? ncclSum : ncclMax, S->comm, S->h->stream));
+    return SW_OK;
+}
+
+/*
+ * The solve's common path with the controller's decisions on the device
+ * (DESIGN.md §7.2): setup, the level search, SELECT at M_lo (its price search,
+ * take and assign), the SELECT / UMAX evaluations, the next level interval's
+ * count, the share placement, the exchange step and the final evaluation are
+ * all enqueued at once — every collective on the stream (RCCL or the peer
+ * transport), every decision a one-wave kernel (k_fast_*) — and the host
+ * reads one result.  The path is sw_shard_solve's whenever the level search
+ * ends at M_lo (no other level can win), the tie group fills the budget (no
+ * width tail) and every share places its counts: then the same kernels on
+ * the same values give the same result bit for bit.  Otherwise the result
+ * says escape and the host-driven controller solves the instance again
+ * (returns 2); 1 = solved; 0 = not attempted; < 0 = error.  Host collectives
+ * keep the host controller (every step needs the host there).
+ */
+int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* res) {
+    static const bool off = getenv("SW_SHARD_NOFAST") != nullptr; /* A/B: the host-driven controller */
+    static const bool trace = getenv("SW_FAST_TRACE") != nullptr; /* diagnostics: sync after each stage */
+#define FAST_TRACE(what)                                                                      \
+    do {                                                                                      \
+        if (trace) {                                                                          \
+            hipError_t e_ = hipStreamSynchronize(S->h->stream);                              \
+            fprintf(stderr, "fast_solve: %s: %s\n", what, hipGetErrorString(e_));           \
+        }                                                                                     \
+    } while (0)
+    if (off || (S->host_comm && !S->peer) || !(N > 0 && pr->regularizer > 0.0)) return 0;
+    hipStream_t st = S->h->stream;
+    const int W = S->world, LW = (int)S->LW;
+    const long long C = (long long)pr->num_gpus * pr->future_rounds;
+    FastCtl* fc = S->fctl.p;
+    unsigned long long* sbL = S->srch.p;     /* the level search's states */
+    unsigned long long* sbP = S->srch.p + 8; /* the price search's */
+    disarm_pub(S);
+    /* setup (op_setup): constants, key rows, the maxima */
+    SH_TRY(zero_red(S, 4));
+    long long* R0 = S->dv.red;
+    LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->in_w, S->in_d, S->in_F, S->in_E,
+           S->in_R, S->delta);
+    SH_TRY(coll_dev_reduce(S, R0, 4, 1));
+    LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv);
+    LAUNCH(S, k_fast_lvl_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R0, sbL, C, pr->regularizer);
+    FAST_TRACE("setup");
+    /* the level search M_lo: ≤ 11 rounds over ≤ 64 bits (closed rounds are empty) */
+    unsigned long long *srl = nullptr, *spf = nullptr;
+    SH_TRY(enqueue_search(S, 1, 11, sbL, &srl));
+    FAST_TRACE("level search");
+    /* SELECT(M_lo) (swc_select): force, the price search, take, assign */
+    SH_TRY(zero_red(S, 2));
+    long long* R1 = S->dv.red;
+    LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl);
+    SH_TRY(coll_dev_reduce(S, R1, 2, 0));
+    LAUNCH(S, k_fast_price_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R1, (const unsigned long long*)srl,
+           sbP);
+    int nrp = 0;
+    for (uint64_t sp = SW_KEY_INF_BITS; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nrp; /* op_search's count */
+    SH_TRY(enqueue_search(S, 0, nrp, sbP, &spf));
+    FAST_TRACE("price search");
+    SH_TRY(zero_red(S, 2));
+    long long* R2 = S->dv.red;
+    LAUNCH(S, k_take, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0u, (const unsigned long long*)spf,
+           (const FastCtl*)fc);
+    const void* gv = R2;
+    if (W > 1) SH_TRY(coll_gather(S, R2, S->xrecv.p, 16, nullptr, &gv));
+    SH_TRY(zero_red(S, 1));
+    long long* R3 = S->dv.red;
+    LAUNCH(S, k_assign, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0ll, 0ll, fc, (const long long*)gv, W);
+    SH_TRY(coll_dev_reduce(S, R3, 1, 0));
+    FAST_TRACE("take/assign");
+    const double* v = nullptr;
+    SH_TRY(eval_enqueue(S, SW_EV_SELECT, 0, &v, nullptr));
+    LAUNCH(S, k_fast_sel_sum, dim3(1), dim3(64), 0, st, fc, v, W, LW);
+    /* swc_level_search after M_lo: the utility optimum, then the level
+     * values in (M_lo, M_lo + wmax] (none: M_lo wins) */
+    SH_TRY(eval_enqueue(S, SW_EV_UMAX, 0, &v, nullptr));
+    LAUNCH(S, k_fast_sel_ctl, dim3(1), dim3(64), 0, st, fc, (const long long*)R3, v,
+           (const unsigned long long*)spf, W, LW);
+    SH_TRY(zero_red(S, 1));
+    long long* R4 = S->dv.red;
+    LAUNCH(S, k_between, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0.0, (const FastCtl*)fc);
+    SH_TRY(coll_dev_reduce(S, R4, 1, 0));
+    SH_TRY(op_copy(S, SW_A_NB, SW_A_N));
+    FAST_TRACE("between");
+    /* the share placement (P1's and, in density order, P2's), then the
+     * exchange step and the final evaluation on it (sw_shard_solve) */
+    SH_TRY(op_pack_share(S, SW_A_NB, SW_Y_CUR, SW_A_PL));
+    SH_TRY(eval_enqueue(S, SW_EV_PACKED, SW_A_PL, &v, nullptr));
+    LAUNCH(S, k_fast_packed, dim3(1), dim3(64), 0, st, fc, v, W, LW);
+    FAST_TRACE("pack");
+    long long* R5 = nullptr;
+    SH_TRY(p2x_enqueue(S, SW_Y_CUR, SW_A_PL, &R5, false));
+    FAST_TRACE("p2x");
+    SH_TRY(eval_enqueue(S, SW_EV_FINAL, SW_Y_CUR, &v, nullptr));
+    SH_TRY(publish_reserve(S, sizeof(FastOut) / 4 + 1));
+    const unsigned long long seq = ++S->pub_seq;
+    LAUNCH(S, k_fast_final, dim3(1), dim3(64), 0, st, (const FastCtl*)fc, (const long long*)R4,
+           (const long long*)R5, v, (const unsigned long long*)srl, (const unsigned long long*)spf, W, LW,
+           reinterpret_cast<FastOut*>(S->pub_dev), S->pub_flag_dev, seq, (const int*)S->xerr);
+    FAST_TRACE("final");
+#undef FAST_TRACE
+    /* one wait for the whole solve */
+    auto t0 = std::chrono::steady_clock::now();
+    uint32_t spins = 0;
+    while (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq) {
+        __builtin_ia32_pause();
+        if (((++spins) & 0xFFFFu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+            SH_HIP(S, hipStreamSynchronize(st));
+            if (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq)
+                return S->h->err = "fast path: the result never arrived", SW_ERR_HIP;
+            break;
+        }
+    }
+    FastOut o;
+    memcpy(&o, S->pub, sizeof(o));
+    if (trace)
+        fprintf(stderr, "fast_solve: escape %d objective %.17g iters %d status %d\n", o.escape, o.objective,
+                o.iters, o.status);
+    if (o.xerr) {
+        S->xfailed = true; /* sticky: the ranks stopped at different exchanges */
+        return S->h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+    }
+    if (o.escape) return 2;
+    res->objective = o.objective;
+    res->utility = o.utility;
+    res->makespan = o.makespan;
+    res->p2_objective = o.p2;
+    res->bound = o.bound;
+    res->iters = o.iters;
+    res->status = o.status;
+    return 1;
+}
+
 int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_t total_jobs,
                sw_result* res, bool dev) {
     if (!h || !res || !local) return SW_ERR_INVALID;
@@ -3028,6 +3419,46 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
         return h->err = "peer exchange timed out earlier: the ranks' sequence numbers diverged, "
                         "rebuild the handle", SW_ERR_RCCL;
     SH_TRY(prepare(S, local, job_offset, total_jobs, dev, res));
+    int rc = fast_solve(S, local, total_jobs, res);
+    if (rc < 0) return rc;
+    if (rc == 1) {
+        rc = SW_OK;
+    } else {
+        rc = slow_solve(S, local, total_jobs, res, rc == 2);
+        if (rc < 0) return rc;
+    }
+    const size_t n = (size_t)S->NL;
+    if (n && !dev) {
+        if (res->plan)
+            SH_HIP(S, hipMemcpyAsync(res->plan, S->plan.p, n * S->T, hipMemcpyDeviceToHost, h->stream));
+        if (res->planned_rounds)
+            SH_HIP(S, hipMemcpyAsync(res->planned_rounds, S->planned.p, n * 4, hipMemcpyDeviceToHost,
+                                     h->stream));
+    }
+    SH_HIP(S, hipStreamSynchronize(h->stream));
+    if (S->peer) { /* a timed-out exchange after the last publish */
+        int e = 0;
+        SH_HIP(S, hipMemcpy(&e, S->xerr, sizeof(int), hipMemcpyDeviceToHost));
+        if (e) {
+            S->xfailed = true; /* sticky: the handle is unusable from here on */
+            return h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+        }
+    }
+    return rc;
+}
+
+/* The host-driven controller (sw_shard_ctl.h) over this engine's ops: every
+ * solve that leaves fast_solve's common path, and every solve on host
+ * collectives.  A fast path that escaped left its state behind: cleared first. */
+int slow_solve(sw_shard_state* S, const sw_problem* local, int64_t total_jobs, sw_result* res, bool dirty) {
+    sw_handle* h = S->h;
+    if (dirty) { /* the state and the ring, as prepare() leaves them (k_zero_state clears the
+                  * ring from S.red: its base, not the last step's slice) */
+        S->dv.red = S->red.p;
+        LAUNCH(S, k_zero_state, dim3(nblk(std::max<int64_t>(S->NL, (int64_t)kRing * kRed))), dim3(kTB), 0,
+               h->stream, S->dv);
+        S->ring_pos = 0;
+    }
     sw_shard_ops ops;
     ops.ctx = S;
     ops.setup = op_setup;
@@ -3054,27 +3485,13 @@ int dist_solve(sw_handle* h, const sw_problem* local, int64_t job_offset, int64_
     ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
     ops.pack_share = op_pack_share;
     ops.share_repair = op_share_repair;
+    static const bool trace = getenv("SW_FAST_TRACE") != nullptr;
+    if (trace) fprintf(stderr, "slow_solve: start (dirty %d)\n", (int)dirty);
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,
                             local->regularizer, &res->objective, &res->utility, &res->makespan,
                             &res->p2_objective, &res->bound, &res->iters, &res->status);
+    if (trace) fprintf(stderr, "slow_solve: rc %d objective %.17g iters %d\n", rc, res->objective, res->iters);
     if (rc < 0) return rc == -1 ? (h->err = "out of host memory", SW_ERR_HIP) : rc;
-    const size_t n = (size_t)S->NL;
-    if (n && !dev) {
-        if (res->plan)
-            SH_HIP(S, hipMemcpyAsync(res->plan, S->plan.p, n * S->T, hipMemcpyDeviceToHost, h->stream));
-        if (res->planned_rounds)
-            SH_HIP(S, hipMemcpyAsync(res->planned_rounds, S->planned.p, n * 4, hipMemcpyDeviceToHost,
-                                     h->stream));
-    }
-    SH_HIP(S, hipStreamSynchronize(h->stream));
-    if (S->peer) { /* a timed-out exchange after the last publish */
-        int e = 0;
-        SH_HIP(S, hipMemcpy(&e, S->xerr, sizeof(int), hipMemcpyDeviceToHost));
-        if (e) {
-            S->xfailed = true; /* sticky: the handle is unusable from here on */
-            return h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
-        }
-    }
     return rc;
 }
 }  // namespace
