@@ -74,9 +74,16 @@ __device__ uint64_t g_sw_pack_stamps[24]; /* swp[0..7] phases, [17..19] counters
 namespace {
 
 constexpr int kTB = 256;  /* threads per block of the per-job kernels */
-constexpr int kRed = 128; /* entries of the step-result buffer        */
+constexpr int kRed = 320; /* entries of a step-result slice (a probe's SW_SHARD_K + 1 bins) */
 constexpr int kRing = 64; /* step-result slices cleared together      */
-constexpr int kProbeBlocks = 256; /* grid of the K-ary probe kernels       */
+constexpr int kProbeBlocks = 256; /* grid of the K-ary price probes (SW_PROBE_BLOCKS overrides; 0 = full) */
+int probe_blocks(unsigned pb) {
+    static const int v = [] {
+        const char* e = getenv("SW_PROBE_BLOCKS");
+        return e ? atoi(e) : kProbeBlocks;
+    }();
+    return (v <= 0 || pb <= (unsigned)v) ? (int)pb : v;
+}
 /* a pack's per-round capacities, passed by value (no staging copy) */
 struct CapsArg {
     int32_t v[SW_TMAX];
@@ -197,7 +204,8 @@ __device__ __forceinline__ void pub_store(const ShardDev& S) {
         __hip_atomic_store(S.pub.flag, S.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-constexpr int kRedCtr = 120; /* a step-result slot no step uses: the last-block counter */
+constexpr int kRedCtr = 300; /* a step-result slot no step uses: the last-block counter */
+static_assert(SW_SHARD_K + 1 <= kRedCtr && kRedCtr < kRed, "the probe bins stay below the counter slot");
 /* At the end of a step kernel, by every thread that did not return: when
  * armed, the last block to finish (counter red[kRedCtr], zero in every fresh
  * step slice) publishes.  Uniform over the grid: S.pub is a kernel argument. */
@@ -385,25 +393,42 @@ __global__ void k_search_init(unsigned long long* sr, unsigned long long lo, uns
  * closed bracket is left as it is). */
 __device__ __forceinline__ void search_step_wave(const unsigned long long* x, const long long* bins,
                                                  unsigned long long* out) {
+    constexpr int PL = (SW_SHARD_K + 63) / 64; /* thresholds per lane: i = PL·lane + j */
     const uint64_t lo = x[0], hi = x[1];
     const int64_t bud = (int64_t)x[2];
     const SearchPts q = search_pts(lo, hi);
-    const int i = lane_id();
+    const int lane = lane_id();
     if (q.K == 0) {
-        if (i < 4) out[i] = x[i];
+        if (lane < 4) out[lane] = x[lane];
         return;
     }
-    int64_t cnt = (i < q.K) ? (int64_t)bins[i + 1] : 0;
+    /* cnt[i] = Σ_{b > i} bins[b]: each lane's suffix over its PL bins, then
+     * an exclusive suffix scan of the lane totals (the same integers) */
+    int64_t c[PL];
+    int64_t tot = 0;
+#pragma unroll
+    for (int j = PL - 1; j >= 0; --j) {
+        const int i = PL * lane + j;
+        tot += (i < q.K) ? (int64_t)bins[i + 1] : 0;
+        c[j] = tot;
+    }
+    int64_t after = tot; /* Σ over the lanes above this one, by a shuffle suffix scan */
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int64_t v = __shfl_down(cnt, o, 64);
-        cnt += (i + o < 64) ? v : 0;
+        const int64_t v = __shfl_down(after, o, 64);
+        after += (lane + o < 64) ? v : 0;
     }
-    const uint64_t ok = __ballot(i < q.K && cnt <= bud);
-    if (i == 0) {
+    after -= tot;
+    int fj = PL;
+#pragma unroll
+    for (int j = PL - 1; j >= 0; --j)
+        if (PL * lane + j < q.K && c[j] + after <= bud) fj = j;
+    const uint64_t ok = __ballot(fj < PL);
+    const int fl = ok ? __builtin_ctzll(ok) : 0;
+    const int f = ok ? PL * fl + __shfl(fj, fl, 64) : q.K;
+    if (lane == 0) {
         uint64_t nlo = lo, nhi = hi;
-        if (ok) {
-            const int f = __builtin_ctzll(ok);
+        if (f < q.K) {
             nhi = search_pt(lo, q, f);
             if (f > 0) nlo = search_pt(lo, q, f - 1) + 1u;
         } else {
@@ -640,25 +665,29 @@ __global__ void k_fill_apply(ShardDev S, int i, int t) {
  * block to finish (counter red[kRedCtr]) copies them behind the lanes.
  * out = [A lanes][B lanes][gm][isum].  SW_EV_FINAL also writes the plan row
  * and count of each job. */
+/* sel = kEvSelUmax (fast_solve): SW_EV_SELECT's A, B, max g and a third
+ * lane sum C = f(T_j) (SW_EV_UMAX's A) in one pass, out = [A][B][gm][isum][C] */
+constexpr int kEvSelUmax = 7;
 __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t* arr,
                                              const uint64_t* ysrc, int arr_a, int arr_b, int lpb,
                                              double* out) {
-    __shared__ double xs[2][kTB];
+    __shared__ double xs[3][kTB];
     __shared__ long long wred[kTB / 64];
     __shared__ unsigned long long wmax[kTB / 64];
     __shared__ int last;
     const int64_t q = S.q;
     const int64_t lane0 = (int64_t)blockIdx.x * lpb;
     const int64_t i = lane0 * q + (int64_t)threadIdx.x; /* local job of this thread */
-    double fa = 0.0, fb = 0.0, gm = 0.0;
+    double fa = 0.0, fb = 0.0, fc = 0.0, gm = 0.0;
     long long is = 0;
     if ((int64_t)threadIdx.x < (int64_t)lpb * q && i < S.NL) {
         const sw_jobc c = S.jc[i];
-        if (sel == SW_EV_SELECT) {
+        if (sel == SW_EV_SELECT || sel == kEvSelUmax) {
             const int n = S.arr[SW_A_N][i];
             fa = sw_f(&c, n, S.nb, S.beta, S.ell, S.slope);
             fb = sw_f(&c, S.l[i] + S.taken[i], S.nb, S.beta, S.ell, S.slope);
             gm = sw_g(&c, n);
+            if (sel == kEvSelUmax) fc = sw_f(&c, tj_of(S, c), S.nb, S.beta, S.ell, S.slope);
         } else if (sel == SW_EV_GMAX) {
             gm = sw_g(&c, arr[i]);
         } else if (sel == SW_EV_PACKED) {
@@ -691,6 +720,7 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
     }
     xs[0][threadIdx.x] = fa;
     xs[1][threadIdx.x] = fb;
+    xs[2][threadIdx.x] = fc;
     /* block max / sum, one atomic each per block */
     const unsigned long long gb = wave_max((unsigned long long)sw_bits(gm)); /* g ≥ 0: bit order = value order */
     const long long sb = wave_sum(is);
@@ -707,13 +737,15 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
     const int64_t lane = lane0 + (int64_t)threadIdx.x;
     if ((int)threadIdx.x < lpb && lane < S.LW) {
         const int64_t jb = lane * q, je = min((int64_t)S.NL, jb + q);
-        double a = 0.0, b = 0.0;
+        double a = 0.0, b = 0.0, cc = 0.0;
         for (int64_t j = jb; j < je; ++j) {
             a = a + xs[0][j - lane0 * q];
             b = b + xs[1][j - lane0 * q];
+            cc = cc + xs[2][j - lane0 * q];
         }
         out[lane] = a;
         out[S.LW + lane] = b;
+        if (sel == kEvSelUmax) out[2 * S.LW + 2 + lane] = cc;
     }
     /* the last block publishes max g and the sum behind the lanes */
     __threadfence();
@@ -746,13 +778,13 @@ __global__ __launch_bounds__(kTB) void k_eval(ShardDev S, int sel, const int32_t
  * partial ℓ of the gathered eval blocks: rank ℓ / LW, offset ℓ mod LW), each
  * chunk halved by shuffles (p[i] + p[i + h], the same operands as the host
  * loop), then the eight chunk sums by the same halving.  Wave-uniform result. */
-__device__ __forceinline__ double wave_tree512(const double* blocks, int blk, int LW, int part) {
+__device__ __forceinline__ double wave_tree512(const double* blocks, int blk, int LW, int off) {
     const int lane = lane_id();
     double ws[SW_DET_LANES / 64];
 #pragma unroll
     for (int w = 0; w < SW_DET_LANES / 64; ++w) {
         const int idx = 64 * w + lane, r = idx / LW, o = idx - r * LW;
-        double v = blocks[(size_t)r * blk + (size_t)part * LW + o];
+        double v = blocks[(size_t)r * blk + (size_t)off + o];
 #pragma unroll
         for (int h = 32; h >= 1; h >>= 1) v = v + __shfl_down(v, h, 64);
         ws[w] = __shfl(v, 0, 64);
@@ -816,30 +848,22 @@ __global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigne
  * (swc_select / swc_level_search); a width tail leaves the common path */
 /* Every gathered view is consumed by the kernel right after its gather (the
  * peer transport's region half is rewritten two exchanges later). */
-__global__ __launch_bounds__(64) void k_fast_sel_sum(FastCtl* c, const double* sel, int W, int LW) {
-    const int blk = 2 * LW + 2;
+__global__ __launch_bounds__(64) void k_fast_sel_ctl(FastCtl* c, const long long* R3, const double* sel,
+                                                     const unsigned long long* sp, int W, int LW) {
+    const int blk = 3 * LW + 2; /* [A][B][gm][isum][C] (kEvSelUmax) */
     const double U = wave_tree512(sel, blk, LW, 0);
-    const double Bt = wave_tree512(sel, blk, LW, 1);
+    const double Bt = wave_tree512(sel, blk, LW, LW);
+    const double Um = wave_tree512(sel, blk, LW, 2 * LW + 2);
     if (lane_id() != 0) return;
     double gm;
     long long is;
     blocks_gm_isum(sel, blk, LW, W, gm, is);
-    c->U = U;
-    c->Mact = gm;
-    c->Umax = Bt; /* the B tree, until k_fast_sel_ctl */
-}
-
-__global__ __launch_bounds__(64) void k_fast_sel_ctl(FastCtl* c, const long long* R3, const double* umax,
-                                                     const unsigned long long* sp, int W, int LW) {
-    const int blk = 2 * LW + 2;
-    const double Um = wave_tree512(umax, blk, LW, 0);
-    if (lane_id() != 0) return;
-    (void)W;
     const int all = c->all;
     if (!all && c->rem - R3[0] > 0) c->escape = 1; /* the width tail: host path */
     const double rho_d = all ? 0.0 : (double)sw_float_of((uint32_t)sp[0]);
     const long long wgt = all ? c->Wall : c->wt;
-    const double U = c->U, Bt = c->Umax;
+    c->U = U;
+    c->Mact = gm;
     c->ubound = Bt + (rho_d * c->A) * (double)(c->bud - wgt);
     c->Umax = Um;
     const double wmax = (Um - U) / c->k;
@@ -871,7 +895,7 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
                                                    unsigned long long hseq, const int* xerr) {
     const int blk = 2 * LW + 2;
     const double U = wave_tree512(fin, blk, LW, 0);
-    const double P2 = wave_tree512(fin, blk, LW, 1);
+    const double P2 = wave_tree512(fin, blk, LW, LW);
     if (lane_id() != 0) return;
     double gm;
     long long any;
@@ -989,29 +1013,45 @@ __global__ __launch_bounds__(kTB) void k_load(ShardDev S, const int32_t* src) {
  * rank·nsub … rank·nsub + nsub − 1.  caps[s·64 + t]; caps[SW_VSHARES·64] = 1
  * when the shares exist (0 < L ≤ G·T), else 0.  One wave; exact 64-bit
  * integers (G·T < 2^31, so S·L_r < 2^62; above that no shares). */
+/* sw_share_caps of share v on one wave: lane t < T gets round t's capacity;
+ * false when the shares do not exist.  Lane r < V computes share r's budget
+ * (one 64-bit division each instead of a loop of them per lane). */
+__device__ __forceinline__ bool share_caps_wave(const long long* loads, int V, int v, int T, long long G,
+                                                int32_t& cap) {
+    const int lane = lane_id();
+    const long long Lr = lane < V ? loads[lane] : 0;
+    long long L = Lr;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) L += __shfl_xor(L, o, 64);
+    const long long C = G * (long long)T;
+    cap = 0;
+    if (!(L > 0 && L <= C && T >= 1 && C < (1ll << 31))) return false;
+    const long long Sl = C - L;
+    const long long gi = lane < V ? Sl * Lr / L : 0; /* share lane's ⌊S·L_r/L⌋ */
+    long long given = gi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) given += __shfl_xor(given, o, 64);
+    const long long rest = Sl - given;
+    const long long B = Lr + gi + (lane < rest ? 1 : 0); /* share lane's budget */
+    long long m = lane < v ? B % T : 0; /* the extras of the shares before v */
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m += __shfl_xor(m, o, 64);
+    const long long cursor = m % T;
+    const long long Bv = __shfl(B, v, 64);
+    const long long base = Bv / T, ext = Bv % T;
+    const long long d = ((long long)lane - cursor + T) % T;
+    cap = (int32_t)(base + (d < ext ? 1 : 0));
+    return true;
+}
+
 __global__ __launch_bounds__(64) void k_share_caps(const long long* loads, int V, int rank, int nsub, int T,
                                                    long long G, int32_t* caps) {
     const int lane = lane_id();
-    long long L = 0;
-    for (int r = 0; r < V; ++r) L += loads[r];
-    const long long C = G * (long long)T;
-    const bool ok = L > 0 && L <= C && T >= 1 && C < (1ll << 31);
-    if (lane == 0) caps[SW_VSHARES * 64] = ok ? 1 : 0;
-    if (!ok) return;
-    const long long Sl = C - L;
-    long long given = 0;
-    for (int r = 0; r < V; ++r) given += Sl * loads[r] / L;
-    const long long rest = Sl - given;
-    long long cursor = 0;
-    for (int r = 0; r < V; ++r) {
-        const long long B = loads[r] + Sl * loads[r] / L + (r < rest ? 1 : 0);
-        const int s = r - rank * nsub;
-        if (s >= 0 && s < nsub && lane < T) {
-            const long long base = B / T, ext = B % T;
-            const long long d = ((long long)lane - cursor + T) % T;
-            caps[s * 64 + lane] = (int32_t)(base + (d < ext ? 1 : 0));
-        }
-        cursor = (cursor + B % T) % T;
+    for (int s = 0; s < nsub; ++s) {
+        int32_t c;
+        const bool ok = share_caps_wave(loads, V, rank * nsub + s, T, G, c);
+        if (s == 0 && lane == 0) caps[SW_VSHARES * 64] = ok ? 1 : 0;
+        if (ok && lane < T) caps[s * 64 + lane] = c;
     }
 }
 
@@ -1370,12 +1410,17 @@ __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pac
  * forms: as two launches (k_pack_rounds_wave, then k_pack_rounds_sel for the
  * shares above wa) the C4 placement paid both kernels' ~68 µs in turn
  * (profiles/r8c4a_*). */
+/* loads (the gathered share loads, V of them): each workgroup computes its
+ * share's capacities itself (share_caps_wave) and stores them to capsd for
+ * the host's share repair, instead of a k_share_caps launch before it */
 __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds_share(ShardDev S, const sw_pack_ent* all, int64_t M,
                                                                 const int32_t* order, uint64_t* ydst,
-                                                                int32_t* pdst, const int32_t* capsd, int wa) {
+                                                                int32_t* pdst, int32_t* capsd, int wa,
+                                                                const long long* loads, int V) {
     __shared__ sw_xchg_t<SW_BLOCK / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
+    __shared__ int okL;
     __shared__ uint64_t xmk[64 * 8];
     sw_blk_t<SW_BLOCK / 64> blk;
     blk.X = &X;
@@ -1383,14 +1428,26 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds_share(ShardDev S, cons
     const int tid = threadIdx.x;
     const int64_t eb = (int64_t)blockIdx.x * M;
     order += eb;
-    if (tid < S.T) capsL[tid] = capsd[blockIdx.x * 64 + tid];
+    if (tid < 64) {
+        int32_t c;
+        const bool ok = share_caps_wave(loads, V, S.rank * S.nsub + blockIdx.x, S.T, S.G, c);
+        if (tid < S.T) {
+            capsL[tid] = c;
+            capsd[blockIdx.x * 64 + tid] = c;
+        }
+        if (tid == 0) {
+            okL = ok;
+            if (blockIdx.x == 0) capsd[SW_VSHARES * 64] = ok ? 1 : 0;
+        }
+    }
     int r0, r1;
     share_rows(S, capsd, 1, r0, r1);
     for (int i = r0 + tid; i < r1; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
-    if (capsd[SW_VSHARES * 64] == 0) return; /* no shares: nothing placed */
+    __syncthreads(); /* capsL, okL */
+    if (!okL) return; /* no shares: nothing placed */
     int act = 0;
     for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[eb + e].st != 0;
-    const int A = blk.sum32(act); /* its barrier publishes capsL and orders the cleared rows first */
+    const int A = blk.sum32(act); /* its barrier orders the cleared rows first */
     if (A <= wa && A <= 64 * 8) {
         if (wave_id() == 0) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, capsL, &PL, xmk);
         return;
@@ -2350,7 +2407,7 @@ int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
     /* the price probe is bound by its block → global flush (K atomics per
      * block): a bounded grid; the level probe by its fp64 work: full grid */
     const unsigned pb = nblk((int64_t)S->NL * S->T);
-    const unsigned grid = (!LEVEL && pb > (unsigned)kProbeBlocks) ? (unsigned)kProbeBlocks : pb;
+    const unsigned grid = LEVEL ? pb : (unsigned)probe_blocks(pb);
     LAUNCH(S, k_probe<LEVEL>, dim3(grid), dim3(kTB), 0, S->h->stream, S->dv, th);
     int64_t bins[SW_SHARD_K + 1];
     SH_TRY(coll_reduce(S, S->dv.red, K + 1, 0, bins));
@@ -2394,7 +2451,7 @@ int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* 
         unsigned long long* xout = sb + 4 * (r & 1);
         if (r == 0) xin = sb;
         if (kind == 0)
-            LAUNCH(S, k_probe_dev<false>, dim3(pb > (unsigned)kProbeBlocks ? (unsigned)kProbeBlocks : pb),
+            LAUNCH(S, k_probe_dev<false>, dim3((unsigned)probe_blocks(pb)),
                    dim3(kTB), 0, st, S->dv, xin, xout, prev);
         else
             LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev);
@@ -2518,7 +2575,7 @@ int op_fill_apply(void* ctx, int64_t jb, int32_t t) {
  * where the gathered blocks are on the device (the peer transport's region
  * half: read it before the second exchange after this one). */
 int eval_enqueue(sw_shard_state* S, int32_t sel, int32_t arg, const double** view, double* hout) {
-    const int64_t LW = S->LW, blk = 2 * LW + 2;
+    const int64_t LW = S->LW, blk = (sel == kEvSelUmax ? 3 : 2) * LW + 2;
     SH_TRY(zero_red(S, 2));
     const int32_t* arr = sel == SW_EV_GMAX || sel == SW_EV_PACKED ? S->arr[arg].p : nullptr;
     const uint64_t* ys = sel == SW_EV_FINAL ? S->y[arg].p : nullptr;
@@ -2586,8 +2643,8 @@ int op_copy_y(void* ctx, int32_t dst, int32_t src) {
  * class-wise repack inside a share (jobs [jlo, jhi), caps = the class's
  * capacities) */
 int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
-             int32_t wc, const int32_t* caps, bool local = false, const int32_t* shares = nullptr,
-             int32_t jlo = 0, int32_t jhi = 0x7FFFFFFF) {
+             int32_t wc, const int32_t* caps, bool local = false, int32_t* shares = nullptr,
+             int32_t jlo = 0, int32_t jhi = 0x7FFFFFFF, const long long* loads = nullptr) {
     hipStream_t st = S->h->stream;
     const int nsub = shares ? S->dv.nsub : 1;
     const int64_t Mg = shares ? S->dv.Pp : (local ? S->P : S->P * S->world); /* entries per workgroup */
@@ -2619,9 +2676,9 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
         if (Mg > (nsub > 1 ? 20 : 64) * SW_BLOCK)
             return S->h->err = "share placement: a share holds more jobs than one workgroup's round loop",
                    SW_ERR_CAPACITY;
-        if (Mg <= 8 * SW_BLOCK) { /* both loop forms in one launch */
+        if (loads) { /* both loop forms in one launch, the capacities computed there */
             LAUNCH(S, k_pack_rounds_share, dim3(nsub), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p, yd, pd,
-                   shares, wa);
+                   shares, wa, loads, nsub * S->world);
             return SW_OK;
         }
         LAUNCH(S, k_pack_rounds_wave, dim3(nsub), dim3(64), 0, st, dv, all, Mg, S->porder.p, yd, pd, capsd, wa, 1,
@@ -2705,9 +2762,15 @@ int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
         long long* lrecv = reinterpret_cast<long long*>(S->xrecv.p);
         SH_TRY(coll_gather(S, S->dv.red, lrecv, (size_t)nsub * 8, nullptr, &lv));
     }
-    LAUNCH(S, k_share_caps, dim3(1), dim3(64), 0, st, (const long long*)lv, nsub * S->world, S->rank, nsub,
-           S->T, (long long)S->dv.G, S->scapsd.p);
-    return pack_any(S, 4, src, 0.0, ydst, pdst, 0, nullptr, true, S->scapsd.p);
+    /* shares of at most 8·512 entries: k_pack_rounds_share computes its
+     * capacities itself; larger ones take k_share_caps and the separate
+     * loop variants */
+    const bool one = S->dv.Pp <= 8 * SW_BLOCK;
+    if (!one)
+        LAUNCH(S, k_share_caps, dim3(1), dim3(64), 0, st, (const long long*)lv, nsub * S->world, S->rank, nsub,
+               S->T, (long long)S->dv.G, S->scapsd.p);
+    return pack_any(S, 4, src, 0.0, ydst, pdst, 0, nullptr, true, S->scapsd.p, 0, 0x7FFFFFFF,
+                    one ? (const long long*)lv : nullptr);
 }
 
 /* twin: e_share_repair — each of this rank's shares whose pack stranded
@@ -2914,7 +2977,7 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
     const size_t NL = (size_t)std::max<int32_t>(S->NL, 1), T = (size_t)S->T;
     const size_t M = std::max<size_t>((size_t)S->P * S->world, (size_t)(nsub * Pp));
     const size_t Mpad = (M + kSortChunk - 1) / kSortChunk * kSortChunk;
-    const size_t xbytes = std::max<size_t>({(size_t)(2 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
+    const size_t xbytes = std::max<size_t>({(size_t)(3 * S->LW + 2) * 8, (size_t)S->P * 4, 16});
     bool bad = S->w.reserve(NL) || S->F.reserve(NL) || S->E.reserve(NL) || S->d.reserve(NL) ||
                S->R.reserve(NL) || S->p.reserve(NL) || S->jc.reserve(NL) || S->keys.reserve(NL * T) ||
                S->l.reserve(NL) || S->taken.reserve(NL) || S->tie.reserve(NL) ||
@@ -3076,11 +3139,12 @@ int sw_dist_init_host(sw_handle* h, const sw_host_comm* comm, int32_t rank, int3
 
 /* Region slot bytes for instances up to `jobs` jobs at world W: the largest
  * step payload — the placement entries (P·24 B), the lane partials
- * ((2·LW + 2)·8 B), the widths (P·4 B) or a ≤ 128-value all-reduce. */
+ * ((3·LW + 2)·8 B with the fast path's third sum), the widths (P·4 B) or a
+ * ≤ kRed-value all-reduce. */
 static long long peer_slot_bytes(int64_t jobs, int32_t W) {
     const int64_t q = std::max<int64_t>(1, (jobs + SW_DET_LANES - 1) / SW_DET_LANES);
     const int64_t LW = SW_DET_LANES / W, P = LW * q;
-    long long b = std::max<long long>({(long long)P * (long long)sizeof(sw_pack_ent), (2 * LW + 2) * 8,
+    long long b = std::max<long long>({(long long)P * (long long)sizeof(sw_pack_ent), (3 * LW + 2) * 8,
                                        P * 4, (long long)kRed * 8});
     return (b + 255) / 256 * 256;
 }
@@ -3303,9 +3367,11 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv);
     LAUNCH(S, k_fast_lvl_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R0, sbL, C, pr->regularizer);
     FAST_TRACE("setup");
-    /* the level search M_lo: ≤ 11 rounds over ≤ 64 bits (closed rounds are empty) */
+    /* the level search M_lo: ≤ 8 rounds over ≤ 64 bits (closed rounds are empty) */
     unsigned long long *srl = nullptr, *spf = nullptr;
-    SH_TRY(enqueue_search(S, 1, 11, sbL, &srl));
+    int nrl = 0; /* ≤ 64 bits of a level's fp64 pattern: the rounds for the widest span */
+    for (uint64_t sp = ~0ull; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nrl;
+    SH_TRY(enqueue_search(S, 1, nrl, sbL, &srl));
     FAST_TRACE("level search");
     /* SELECT(M_lo) (swc_select): force, the price search, take, assign */
     SH_TRY(zero_red(S, 2));
@@ -3329,12 +3395,10 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     LAUNCH(S, k_assign, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0ll, 0ll, fc, (const long long*)gv, W);
     SH_TRY(coll_dev_reduce(S, R3, 1, 0));
     FAST_TRACE("take/assign");
+    /* the SELECT evaluation and swc_level_search's utility optimum in one
+     * pass, then the level values in (M_lo, M_lo + wmax] (none: M_lo wins) */
     const double* v = nullptr;
-    SH_TRY(eval_enqueue(S, SW_EV_SELECT, 0, &v, nullptr));
-    LAUNCH(S, k_fast_sel_sum, dim3(1), dim3(64), 0, st, fc, v, W, LW);
-    /* swc_level_search after M_lo: the utility optimum, then the level
-     * values in (M_lo, M_lo + wmax] (none: M_lo wins) */
-    SH_TRY(eval_enqueue(S, SW_EV_UMAX, 0, &v, nullptr));
+    SH_TRY(eval_enqueue(S, kEvSelUmax, 0, &v, nullptr));
     LAUNCH(S, k_fast_sel_ctl, dim3(1), dim3(64), 0, st, fc, (const long long*)R3, v,
            (const unsigned long long*)spf, W, LW);
     SH_TRY(zero_red(S, 1));

@@ -32,7 +32,8 @@
  * searches: one step evaluates up to SW_SHARD_K thresholds and one
  * all-reduce carries all K counts.  The predicate is monotone, so the K-ary
  * search returns exactly the bisection's answer in ⌈bits / log2(K+1)⌉ steps
- * (31 → 6 for the price, ≤ 64 → 11 for the level).
+ * (K = 255: 31 → 4 for the price, ≤ 64 → 8 for the level; 63 thresholds took
+ * 6 and 11).
  */
 #ifndef SW_SHARD_CTL_H
 #define SW_SHARD_CTL_H
@@ -45,7 +46,7 @@
 #include "sw_bnb.h"
 #include "sw_repair.h"
 
-#define SW_SHARD_K 63 /* thresholds evaluated per search step (≤ 63) */
+#define SW_SHARD_K 255 /* thresholds evaluated per search step (≤ 255: one per thread of a probe block) */
 #define SW_CLASS_HIST (-2) /* class_caps: the class's count histogram */
 
 /* per-job count arrays an engine keeps for its jobs */
