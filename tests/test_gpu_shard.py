@@ -348,3 +348,28 @@ def test_gpu_workspace_resolve_paths_match_twin(rccl_solver, twin, shard_lib):
                               f"dist W=2 seed {seed} N {N}")
     s.close()
     assert rep >= 2, rep
+
+
+def test_gpu_rccl_world2_on_one_device():
+    """The RCCL transport above world 1 on a one-GPU box:
+    two processes on cuda:0 call sw_dist_init at world 2.  This image's RCCL
+    refuses two ranks on one device (ncclCommInitRank: invalid usage, both
+    ranks, no hang — profiles/r8_rccl_two_ranks_one_gpu.json); if a build
+    accepts them, the sharded solve over RCCL must equal the CPU shard engine
+    at world 2 bit for bit (tools/rccl_same_device.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_same_device.py")],
+                         capture_output=True, text=True, timeout=170)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    inits = [r["init"] for r in line["ranks"]]
+    if inits == ["ok", "ok"]:
+        assert line["twin_equal"], line
+    else:
+        assert inits == ["refused", "refused"], line
+        assert all("ncclCommInitRank" in r["error"] for r in line["ranks"]), line
