@@ -115,8 +115,11 @@ def assemble(a, parts):
 
 P1_BITS = sn.SW_STATUS_P1_REPACKED | sn.SW_STATUS_NO_PLANNED | sn.SW_STATUS_P1_UNCERTIFIED
 # the share placement's P2 against the single instance's (both after the
-# exchange step): ≤ 1.002 measured over these cases, the fuzz set and C4
-SHARE_P2_RATIO = 1.005
+# exchange step), and against the HiGHS optimum of the reference P2 MILP on
+# the large fixtures: worst measured 1.00196 (case N1500 at W = 8) and
+# 1.00158 (the 3,000-job fixture at W = 8) — the reference's own P2 gap is
+# 1e-3 (shockwave.py:405), so 1.002 is its bar plus the measured margin
+SHARE_P2_RATIO = 1.002
 
 
 def assert_share_contract(rs, rt, what):
