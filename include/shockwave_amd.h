@@ -217,14 +217,30 @@ int sw_kernel_times(sw_handle* h, double* ms_p2x, double* ms_plan, int32_t* runs
  *
  * Every step of the solve is a pass over the rank's jobs plus one collective:
  * per-round demand / price-step counts and the makespan are all-reduced, the
- * deterministic-sum lane partials and the placement keys are all-gathered
- * (DESIGN.md §7).  Collectives run on RCCL over xGMI (sw_dist_init) or on
- * caller-supplied host collectives (sw_dist_init_host, e.g. gloo).
+ * deterministic-sum lane partials are all-gathered.  On RCCL
+ * or the peer transport the whole common path is enqueued at once, with the
+ * controller's decisions taken on the device, and the host reads one result.
+ * Collectives run on RCCL over xGMI (sw_dist_init), peer memory
+ * (sw_dist_enable_peer) or caller-supplied host collectives
+ * (sw_dist_init_host, e.g. gloo).
  *
  * Sharding rule: world must divide 512 (1, 2, 4, … 512) and rank r must hold
- * exactly the jobs sw_dist_shard_range(total_jobs, world, r) returns.  With
- * that rule the result (plan rows, counts, objective bits) is identical to
- * sw_plan_solve on the whole instance, for every world size.
+ * exactly the jobs sw_dist_shard_range(total_jobs, world, r) returns.
+ *
+ * The result contract.  The plan is placed in V shares —
+ * V = 8 for instances of 4,096 … 65,536 jobs on at least 512 GPUs at every
+ * world ≤ 8, else V = world — each share's jobs alone in the share's part of
+ * every round.  So:
+ *   - P1 (planned_rounds, objective, utility, makespan, bound, the P1 status
+ *     bits) is sw_plan_solve's on the whole instance, bit for bit, at every
+ *     world size (or better, when only the shares place the level search's
+ *     counts);
+ *   - the plan rows and p2_objective are sw_plan_solve's when V = 1, and
+ *     otherwise depend on V only, not on the world size: a large instance
+ *     gives one result at worlds 1, 2, 4 and 8; P2 stays within 1.002 of the
+ *     single instance's (tests/test_shard.py SHARE_P2_RATIO);
+ *   - at every world the result equals the CPU shard engine
+ *     (oracle/shard_twin.c) bit for bit.
  *
  * unique_id points to SW_NCCL_UNIQUE_ID_BYTES bytes produced by
  * sw_dist_unique_id() on rank 0 and broadcast by the caller.  local describes

@@ -17,10 +17,27 @@ replaced by
 
 The result is clipped to [0, 1] as ``x.value.clip(min=0.0).clip(max=1.0)``
 (max_min_fairness.py:100).  A native error raises; there is no CPU fallback.
+
+Known divergence (several worker types): where the LP's optimum is not
+unique — typical for max-min LPs, and certain for the unit-throughput
+``MaxMinFairnessPolicy`` with identical types — the per-job, per-type shares
+are a vertex of the optimal face, not ECOS's interior point: the level t* is
+the same, the split over jobs and types may differ.  The first such call
+warns (``SimplexVertexWarning``); parity is unpinned (ECOS is absent here).
+The simulator and every BASELINE configuration use one worker type.
 """
+import warnings
+
 import numpy as np
 
 import sw_native
+
+
+class SimplexVertexWarning(UserWarning):
+    """The heterogeneous allocation is an optimal vertex, not ECOS's interior point."""
+
+
+_WARNED = False
 
 
 def _flatten(d, cluster_spec):
@@ -94,6 +111,13 @@ class MaxMinFairnessPolicyWithPerf:
             x, _, _ = eng.mmf_allocate(sf, coef[:, 0], int(num_workers[0]))
             x = x.reshape(-1, 1)
         else:
+            global _WARNED
+            if not _WARNED:
+                _WARNED = True
+                warnings.warn("MaxMinFairness over several worker types returns an optimal vertex of the "
+                              "LP (GPU simplex); the reference's ECOS returns an interior point of the same "
+                              "optimal face, so shares may differ where the optimum is not unique",
+                              SimplexVertexWarning, stacklevel=2)
             x, _, _ = eng.mmf_allocate_types(num_workers, sf, coef)
         return _unflatten(x.clip(min=0.0).clip(max=1.0), index)
 
