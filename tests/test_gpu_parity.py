@@ -110,3 +110,29 @@ def test_gpu_rejects_invalid(gpu_solver):
     a = sn.ProblemArrays([0], [1.0], [0], [1], [1.0], [1.0], 4, 2, 120.0, 1.0)
     with pytest.raises(sn.NativeError):
         gpu_solver.solve(a)
+
+
+def test_gpu_resolve_with_job_indices_above_65535(gpu_solver, twin):
+    """A re-solved instance (SW_STATUS_P1_REPACKED: the per-round
+    re-optimisation runs) whose active jobs sit at indices ≥ 66,000 — 66,000
+    finished jobs first, then a 40-job width-fragmented instance — so the
+    knapsack's items carry job indices above 16 bits (sw_reround_dev.h keeps
+    the full index).  The workspace path of sw_plan_solve equals
+    the twin bit for bit."""
+    import sw_native as sn
+    import sw_synth as ss
+
+    b = ss.synth_problem(0, 40, 12, 12, 120.0, 1.0, 5.0, width_p=(0.4, 0.3, 0.2, 0.1))
+    pad = 66000
+    a = sn.ProblemArrays(np.concatenate([np.ones(pad, np.int32), b.w]),
+                         np.concatenate([np.full(pad, 1.0), b.d]),
+                         np.concatenate([np.full(pad, 10, np.int32), b.F]),
+                         np.concatenate([np.full(pad, 10, np.int32), b.E]),
+                         np.concatenate([np.zeros(pad), b.R]), np.concatenate([np.zeros(pad), b.p]),
+                         b.T, b.G, b.delta, b.k, tuple(b.bases))
+    rt = twin.solve(a)
+    assert rt["status"] & sn.SW_STATUS_P1_REPACKED
+    assert rt["planned_rounds"][pad:].sum() > 0 and rt["planned_rounds"][:pad].sum() == 0
+    rg = gpu_solver.solve(a)
+    check_plan_valid(a, rg)
+    assert_same_result(rg, rt, "N=66040 re-solved")
