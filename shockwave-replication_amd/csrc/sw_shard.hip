@@ -257,7 +257,12 @@ __global__ __launch_bounds__(kTB) void k_setup(ShardDev S, sw_jobc* jc, const in
  * so any scan order gives the sequential loop's values), the fp32 keys
  * stored coalesced.  (A thread per job walked its 30 rounds in sequence:
  * 16 µs per C4 solve, the job loop spread over only NL / 256 workgroups.) */
-__global__ __launch_bounds__(kTB) void k_keys(ShardDev S) {
+/* fc (fast_solve): thread 0 of block 0 also sets up the level search
+ * (k_fast_lvl_init's work, from the same setup result) */
+__device__ void fast_lvl_init(FastCtl* c, const long long* R0, unsigned long long* sr, long long C, double k);
+__global__ __launch_bounds__(kTB) void k_keys(ShardDev S, FastCtl* fc = nullptr, unsigned long long* sr = nullptr,
+                                             long long C = 0, double kk = 0.0) {
+    if (fc && blockIdx.x == 0 && threadIdx.x == 0) fast_lvl_init(fc, S.red, sr, C, kk);
     const int64_t i = ((int64_t)blockIdx.x * kTB + threadIdx.x) >> 6;
     if (i >= S.NL) return; /* uniform over the wave */
     const int n = lane_id();
@@ -809,8 +814,7 @@ __device__ __forceinline__ void blocks_gm_isum(const double* blocks, int blk, in
 }
 
 /* after setup: the level search's bracket [lb, top) and budget C */
-__global__ void k_fast_lvl_init(FastCtl* c, const long long* R0, unsigned long long* sr, long long C, double k) {
-    if (threadIdx.x != 0) return;
+__device__ void fast_lvl_init(FastCtl* c, const long long* R0, unsigned long long* sr, long long C, double k) {
     FastCtl z;
     memset(&z, 0, sizeof(z));
     z.C = C;
@@ -892,7 +896,7 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
                                                    const long long* R5, const double* fin,
                                                    const unsigned long long* srl, const unsigned long long* sp,
                                                    int W, int LW, FastOut* hout, unsigned long long* hflag,
-                                                   unsigned long long hseq, const int* xerr) {
+                                                   unsigned long long hseq, const int* xerr, const long long* Rd) {
     const int blk = 2 * LW + 2;
     const double U = wave_tree512(fin, blk, LW, 0);
     const double P2 = wave_tree512(fin, blk, LW, LW);
@@ -901,7 +905,8 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
     long long any;
     blocks_gm_isum(fin, blk, LW, W, gm, any);
     FastOut o;
-    o.escape = c->escape || (c->did_between && R4[0] != 0); /* the branch and bound: host path */
+    o.escape = c->escape || (c->did_between && R4[0] != 0) /* the branch and bound: host path */
+               || (Rd && Rd[0] != 0);                        /* stranded rounds: the share repair */
     o.utility = U;
     o.p2 = P2;
     o.makespan = gm;
@@ -1413,10 +1418,14 @@ __global__ __launch_bounds__(NT) void k_pack_rounds_sel(ShardDev S, const sw_pac
 /* loads (the gathered share loads, V of them): each workgroup computes its
  * share's capacities itself (share_caps_wave) and stores them to capsd for
  * the host's share repair, instead of a k_share_caps launch before it */
+/* dfc (fast_solve): Σ w·(nsrc − placed) over the share's rows — the
+ * PACKED evaluation's stranded rounds — added to *dfc by each workgroup */
 __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds_share(ShardDev S, const sw_pack_ent* all, int64_t M,
                                                                 const int32_t* order, uint64_t* ydst,
                                                                 int32_t* pdst, int32_t* capsd, int wa,
-                                                                const long long* loads, int V) {
+                                                                const long long* loads, int V,
+                                                                const int32_t* nsrc = nullptr,
+                                                                long long* dfc = nullptr) {
     __shared__ sw_xchg_t<SW_BLOCK / 64> X;
     __shared__ sw_pack_lds PL;
     __shared__ int32_t capsL[64];
@@ -1444,17 +1453,35 @@ __global__ __launch_bounds__(SW_BLOCK) void k_pack_rounds_share(ShardDev S, cons
     share_rows(S, capsd, 1, r0, r1);
     for (int i = r0 + tid; i < r1; i += SW_BLOCK) { ydst[i] = 0; pdst[i] = 0; }
     __syncthreads(); /* capsL, okL */
-    if (!okL) return; /* no shares: nothing placed */
-    int act = 0;
-    for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[eb + e].st != 0;
-    const int A = blk.sum32(act); /* its barrier orders the cleared rows first */
-    if (A <= wa && A <= 64 * 8) {
-        if (wave_id() == 0) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, capsL, &PL, xmk);
-        return;
+    if (okL) { /* no shares: nothing placed */
+        int act = 0;
+        for (int64_t e = tid; e < M; e += SW_BLOCK) act += all[eb + e].st != 0;
+        const int A = blk.sum32(act); /* its barrier orders the cleared rows first */
+        if (A <= wa && A <= 64 * 8) {
+            if (wave_id() == 0) pack_rounds_wave_body<8>(S, all, A, order, ydst, pdst, capsL, &PL, xmk);
+        } else if (A <= 2 * SW_BLOCK) {
+            pack_rounds_body<2>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+        } else if (A <= 4 * SW_BLOCK) {
+            pack_rounds_body<4>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+        } else if (A <= 8 * SW_BLOCK) {
+            pack_rounds_body<8>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+        }
     }
-    if (A <= 2 * SW_BLOCK) pack_rounds_body<2>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
-    else if (A <= 4 * SW_BLOCK) pack_rounds_body<4>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
-    else if (A <= 8 * SW_BLOCK) pack_rounds_body<8>(S, all, A, order, ydst, pdst, true, blk, &PL, capsL);
+    if (!dfc) return;
+    __syncthreads(); /* the share's rows are final (device-scope loads below: no stale L1 lines) */
+    long long v = 0;
+    for (int i = r0 + tid; i < r1; i += SW_BLOCK)
+        v += (long long)S.jc[i].w *
+             (nsrc[i] - __hip_atomic_load(pdst + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v = wave_sum(v);
+    __shared__ long long vs[SW_BLOCK / 64];
+    if (lane_id() == 0) vs[wave_id()] = v;
+    __syncthreads();
+    if (tid == 0) {
+        long long t = 0;
+        for (int w = 0; w < SW_BLOCK / 64; ++w) t += vs[w];
+        if (t) atomicAdd((unsigned long long*)dfc, (unsigned long long)t);
+    }
 }
 
 /* ---- P2 exchange step (sw_p2x_dev.h) on the gathered placement ------------------ */
@@ -1467,16 +1494,31 @@ struct p2x_ent {
 };
 static_assert(sizeof(p2x_ent) == sizeof(sw_pack_ent), "p2x entries reuse the pack's gather buffer");
 
+/* bcnt (world 1: the entries are the gathered ones): also k_p2x_cnt's work
+ * — each workgroup's active entries, and the zeroed width map and counts */
 __global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, const int32_t* n,
-                                                 p2x_ent* out) {
+                                                 p2x_ent* out, int32_t* bcnt = nullptr, uint32_t* wmap = nullptr,
+                                                 int32_t* wcnt = nullptr) {
     const int i = blockIdx.x * kTB + threadIdx.x;
-    if (i >= S.P) return;
     p2x_ent e;
     e.m = 0; e.p = 0.0; e.n = 0; e.w = 0;
     if (i < S.NL) {
         e.m = y[i]; e.p = S.p[i]; e.n = n[i]; e.w = S.jc[i].w;
     }
-    out[i] = e;
+    if (i < S.P) out[i] = e;
+    if (!bcnt) return;
+    if (blockIdx.x == 0 && threadIdx.x < 8) wmap[threadIdx.x] = 0u;
+    if (blockIdx.x == 0) wcnt[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) wcnt[256] = 0;
+    const int w = __popcll(__ballot(i < S.P && e.n > 0));
+    __shared__ int32_t ws_[kTB / 64];
+    if (lane_id() == 0) ws_[wave_id()] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int c = 0;
+        for (int k = 0; k < kTB / 64; ++k) c += ws_[k];
+        bcnt[blockIdx.x] = c;
+    }
 }
 
 /* ---- the step's set-up by several workgroups (sw_p2x_pre, sw_p2x_dev.h):
@@ -1490,9 +1532,11 @@ __global__ __launch_bounds__(kTB) void k_p2x_ent(ShardDev S, const uint64_t* y, 
  * k_p2x_compact places them (each block's offset = the counts before it),
  * and collects the widths present (wmap) */
 __global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, int32_t* bcnt,
-                                                 uint32_t* wmap) {
+                                                 uint32_t* wmap, int32_t* wcnt) {
     const int64_t j = (int64_t)blockIdx.x * kTB + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 8) wmap[threadIdx.x] = 0u; /* k_p2x_compact ORs into it */
+    if (blockIdx.x == 0) wcnt[threadIdx.x] = 0; /* …and adds widths / its finish counter (wcnt[256]) */
+    if (blockIdx.x == 0 && threadIdx.x == 0) wcnt[256] = 0;
     const int a = (j < M && all[j].n > 0) ? 1 : 0;
     const int w = __popcll(__ballot(a));
     __shared__ int32_t ws_[kTB / 64];
@@ -1505,12 +1549,20 @@ __global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, 
     }
 }
 
+/* …and the width classes (ascending) with their sizes and offsets in hdr,
+ * by the last workgroup to finish (what k_p2x_classes computed from wmap
+ * and a pass over the entries, here from the workgroups' width counts
+ * wcnt[w]: the same integers, one launch fewer) */
 __global__ __launch_bounds__(kTB) void k_p2x_compact(const p2x_ent* all, int64_t M, const int32_t* bcnt,
-                                                     unsigned char* ws, uint32_t* wmap, int32_t* hdr) {
+                                                     unsigned char* ws, uint32_t* wmap, int32_t* hdr,
+                                                     int32_t* wcnt, int T) {
     __shared__ int32_t base_, wsum[kTB / 64];
     __shared__ uint32_t bm[8]; /* this block's widths, one global OR per word */
+    __shared__ int32_t wh[256]; /* this block's active entries per width */
+    __shared__ int last_;
     const int64_t j = (int64_t)blockIdx.x * kTB + threadIdx.x;
     if (threadIdx.x < 8) bm[threadIdx.x] = 0u;
+    wh[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         int b = 0;
         for (unsigned i = 0; i < blockIdx.x; ++i) b += bcnt[i];
@@ -1525,21 +1577,61 @@ __global__ __launch_bounds__(kTB) void k_p2x_compact(const p2x_ent* all, int64_t
     const int lane = lane_id();
     if (lane == 0) wsum[wave_id()] = __popcll(bal);
     __syncthreads();
-    if (act) atomicOr(&bm[(e.w >> 5) & 7], 1u << (e.w & 31));
+    if (act) {
+        atomicOr(&bm[(e.w >> 5) & 7], 1u << (e.w & 31));
+        atomicAdd(&wh[e.w & 255], 1);
+    }
     __syncthreads();
     if (threadIdx.x < 8 && bm[threadIdx.x]) atomicOr(&wmap[threadIdx.x], bm[threadIdx.x]);
-    if (!act) return;
-    int a = base_ + __popcll(bal & ((1ull << lane) - 1ull));
-    for (int i = 0; i < wave_id(); ++i) a += wsum[i];
-    sw_p2x_arrays X;
-    X.cc = reinterpret_cast<double*>(ws);
-    X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
-    X.cw = reinterpret_cast<int32_t*>(X.cm + M);
-    X.cj = X.cw + M;
-    X.cw[a] = e.w;
-    X.cj[a] = (int32_t)j;
-    X.cc[a] = e.p / (double)e.n;
-    X.cm[a] = e.m;
+    if (wh[threadIdx.x]) atomicAdd(&wcnt[threadIdx.x], wh[threadIdx.x]);
+    if (act) {
+        int a = base_ + __popcll(bal & ((1ull << lane) - 1ull));
+        for (int i = 0; i < wave_id(); ++i) a += wsum[i];
+        sw_p2x_arrays X;
+        X.cc = reinterpret_cast<double*>(ws);
+        X.cm = reinterpret_cast<uint64_t*>(X.cc + M);
+        X.cw = reinterpret_cast<int32_t*>(X.cm + M);
+        X.cj = X.cw + M;
+        X.cw[a] = e.w;
+        X.cj[a] = (int32_t)j;
+        X.cc[a] = e.p / (double)e.n;
+        X.cm[a] = e.m;
+    }
+    /* the last workgroup to finish: the classes */
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last_ = atomicAdd(&wcnt[256], 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last_ || threadIdx.x != 0) return;
+    __threadfence();
+    uint32_t wm[8];
+    int K = 0;
+    for (int i = 0; i < 8; ++i) {
+        wm[i] = __hip_atomic_load(&wmap[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        K += __builtin_popcount(wm[i]);
+    }
+    int32_t cls[SW_P2X_KMAX];
+    if (K > SW_P2X_KMAX) {
+        K = -1;
+    } else {
+        K = 0;
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t b = wm[i]; b; b &= b - 1) cls[K++] = 32 * i + __builtin_ctz(b);
+    }
+    hdr[SW_P2X_HDR_K] = K;
+    int o = 0, b = 0;
+    for (int k = 0; k < SW_P2X_KMAX; ++k) {
+        const int m = (K >= 0 && k < K) ? __hip_atomic_load(&wcnt[cls[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0;
+        hdr[SW_P2X_HDR_WC + k] = (K >= 0 && k < K) ? cls[k] : 0;
+        hdr[SW_P2X_HDR_M + k] = m;
+        hdr[SW_P2X_HDR_OFF + k] = o;
+        hdr[SW_P2X_HDR_NW + k] = (m + 63) / 64;
+        hdr[SW_P2X_HDR_BOFF + k] = b;
+        o += m;
+        b += ((m + 63) / 64) * T; /* word offsets, as sw_p2x_block's boff */
+    }
+    hdr[SW_P2X_HDR_OFF + SW_P2X_KMAX] = o;
 }
 
 /* one workgroup: the width classes (ascending) and their sizes, hdr */
@@ -2644,7 +2736,8 @@ int op_copy_y(void* ctx, int32_t dst, int32_t src) {
  * capacities) */
 int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t ydst, int32_t pdst,
              int32_t wc, const int32_t* caps, bool local = false, int32_t* shares = nullptr,
-             int32_t jlo = 0, int32_t jhi = 0x7FFFFFFF, const long long* loads = nullptr) {
+             int32_t jlo = 0, int32_t jhi = 0x7FFFFFFF, const long long* loads = nullptr,
+             long long* dfc = nullptr) {
     hipStream_t st = S->h->stream;
     const int nsub = shares ? S->dv.nsub : 1;
     const int64_t Mg = shares ? S->dv.Pp : (local ? S->P : S->P * S->world); /* entries per workgroup */
@@ -2678,7 +2771,7 @@ int pack_any(sw_shard_state* S, int32_t mode, int32_t src, double Mb, int32_t yd
                    SW_ERR_CAPACITY;
         if (loads) { /* both loop forms in one launch, the capacities computed there */
             LAUNCH(S, k_pack_rounds_share, dim3(nsub), dim3(SW_BLOCK), 0, st, dv, all, Mg, S->porder.p, yd, pd,
-                   shares, wa, loads, nsub * S->world);
+                   shares, wa, loads, nsub * S->world, (const int32_t*)S->arr[src].p, dfc);
             return SW_OK;
         }
         LAUNCH(S, k_pack_rounds_wave, dim3(nsub), dim3(64), 0, st, dv, all, Mg, S->porder.p, yd, pd, capsd, wa, 1,
@@ -2751,8 +2844,16 @@ int op_pack(void* ctx, int32_t mode, int32_t src, double Mb, int32_t ydst, int32
 /* twin: e_pack_share (oracle/shard_twin.c) — the shares' loads all-gathered,
  * every share's capacities computed on the device (k_share_caps), this
  * rank's shares placed side by side, one workgroup each: no host round trip */
+int pack_share_any(sw_shard_state* S, int32_t src, int32_t ydst, int32_t pdst, long long** dfc);
+
 int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
-    auto* S = (sw_shard_state*)ctx;
+    return pack_share_any((sw_shard_state*)ctx, src, ydst, pdst, nullptr);
+}
+
+/* dfc (fast_solve): a zeroed step slot that receives Σ w·(src − placed) over
+ * this rank's rows, summed by the loop kernel (one-launch shares only; else
+ * nullptr comes back and the caller evaluates PACKED) */
+int pack_share_any(sw_shard_state* S, int32_t src, int32_t ydst, int32_t pdst, long long** dfc) {
     hipStream_t st = S->h->stream;
     const int nsub = S->dv.nsub;
     SH_TRY(zero_red(S, nsub));
@@ -2769,8 +2870,17 @@ int op_pack_share(void* ctx, int32_t src, int32_t ydst, int32_t pdst) {
     if (!one)
         LAUNCH(S, k_share_caps, dim3(1), dim3(64), 0, st, (const long long*)lv, nsub * S->world, S->rank, nsub,
                S->T, (long long)S->dv.G, S->scapsd.p);
+    long long* slot = nullptr;
+    if (dfc) {
+        *dfc = nullptr;
+        if (one) {
+            SH_TRY(zero_red(S, 1));
+            slot = S->dv.red;
+            *dfc = slot;
+        }
+    }
     return pack_any(S, 4, src, 0.0, ydst, pdst, 0, nullptr, true, S->scapsd.p, 0, 0x7FFFFFFF,
-                    one ? (const long long*)lv : nullptr);
+                    one ? (const long long*)lv : nullptr, slot);
 }
 
 /* twin: e_share_repair — each of this rank's shares whose pack stranded
@@ -2851,9 +2961,32 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc
 int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, bool arm) {
     hipStream_t st = S->h->stream;
     const int64_t M = S->P * S->world;
-    if (S->p2ws.reserve((size_t)M * SW_P2X_ARR_BYTES)) return host_fail(S, "P2 exchange workspace");
     p2x_ent* mine = reinterpret_cast<p2x_ent*>(S->pall.p + (size_t)S->rank * S->P);
-    LAUNCH(S, k_p2x_ent, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, S->y[ysrc].p, S->arr[nsrc].p, mine);
+    const int T = S->T;
+    const bool prepared = M > SW_BLOCK && M <= SW_P2X_AMAX * 4;
+    /* workspace after the X arrays (prepared set-up): hdr, ord, pc, bitsets, Wb, Wk, block counts,
+     * width counts */
+    const size_t xa = ((size_t)M * SW_P2X_ARR_BYTES + 15) & ~(size_t)15;
+    const size_t words = (size_t)T * ((size_t)(M + 63) / 64 + SW_P2X_KMAX);
+    const size_t need = xa + 256 + (size_t)M * 4 + (size_t)M * 8 + words * 8 +
+                        (size_t)SW_P2X_KMAX * T * T * 9 + 64 + (size_t)nblk(M) * 4 + 16 + 257 * 4 + 16;
+    if (S->p2ws.reserve(prepared ? need : (size_t)M * SW_P2X_ARR_BYTES) || (prepared && S->p2keys.reserve((size_t)M)))
+        return host_fail(S, "P2 exchange workspace");
+    unsigned char* base = S->p2ws.p + xa;
+    int32_t* hdr = reinterpret_cast<int32_t*>(base);
+    int32_t* ord = reinterpret_cast<int32_t*>(base + 256);
+    double* pc = reinterpret_cast<double*>(base + 256 + (((size_t)M * 4 + 15) & ~(size_t)15));
+    uint64_t* B = reinterpret_cast<uint64_t*>(pc + M);
+    double* Wb = reinterpret_cast<double*>(B + words);
+    int8_t* Wk = reinterpret_cast<int8_t*>(Wb + (size_t)SW_P2X_KMAX * T * T);
+    int32_t* bcnt = reinterpret_cast<int32_t*>(Wk + (size_t)SW_P2X_KMAX * T * T);
+    uint32_t* wmap = reinterpret_cast<uint32_t*>(hdr + SW_P2X_HDR_INTS);
+    const int nb = nblk(M);
+    int32_t* wcnt = bcnt + nb; /* 256 width counts + the finish counter */
+    /* world 1: nothing to gather, so the entry kernel also counts (k_p2x_cnt) */
+    const bool fold = prepared && S->world == 1 && nblk(S->P) == nb;
+    LAUNCH(S, k_p2x_ent, dim3(nblk(S->P)), dim3(kTB), 0, st, S->dv, S->y[ysrc].p, S->arr[nsrc].p, mine,
+           fold ? bcnt : nullptr, fold ? wmap : nullptr, fold ? wcnt : nullptr);
     const void* gv = nullptr;
     SH_TRY(coll_gather(S, mine, S->pall.p, (size_t)S->P * sizeof(p2x_ent), nullptr, &gv));
     SH_TRY(zero_red(S, 1));
@@ -2864,30 +2997,10 @@ int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, 
      * starts from the prepared state */
     sw_p2x_pre pre;
     memset(&pre, 0, sizeof(pre));
-    const int T = S->T;
-    const bool prepared = M > SW_BLOCK && M <= SW_P2X_AMAX * 4;
     if (prepared) {
-        /* workspace after the X arrays: hdr, ord, pc, bitsets, Wb, Wk */
-        const size_t xa = ((size_t)M * SW_P2X_ARR_BYTES + 15) & ~(size_t)15;
-        const size_t words = (size_t)T * ((size_t)(M + 63) / 64 + SW_P2X_KMAX);
-        const size_t need = xa + 256 + (size_t)M * 4 + (size_t)M * 8 + words * 8 +
-                            (size_t)SW_P2X_KMAX * T * T * 9 + 64 + (size_t)nblk(M) * 4 + 16;
-        if (S->p2ws.reserve(need) || S->p2keys.reserve((size_t)M))
-            return host_fail(S, "P2 exchange workspace");
-        unsigned char* base = S->p2ws.p + xa;
-        int32_t* hdr = reinterpret_cast<int32_t*>(base);
-        int32_t* ord = reinterpret_cast<int32_t*>(base + 256);
-        double* pc = reinterpret_cast<double*>(base + 256 + (((size_t)M * 4 + 15) & ~(size_t)15));
-        uint64_t* B = reinterpret_cast<uint64_t*>(pc + M);
-        double* Wb = reinterpret_cast<double*>(B + words);
-        int8_t* Wk = reinterpret_cast<int8_t*>(Wb + (size_t)SW_P2X_KMAX * T * T);
-        int32_t* bcnt = reinterpret_cast<int32_t*>(Wk + (size_t)SW_P2X_KMAX * T * T);
-        uint32_t* wmap = reinterpret_cast<uint32_t*>(hdr + SW_P2X_HDR_INTS);
-        const int nb = nblk(M);
-        LAUNCH(S, k_p2x_cnt, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, wmap);
+        if (!fold) LAUNCH(S, k_p2x_cnt, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, wmap, wcnt);
         LAUNCH(S, k_p2x_compact, dim3(nb), dim3(kTB), 0, st, (const p2x_ent*)gv, M, bcnt, S->p2ws.p, wmap,
-               hdr);
-        LAUNCH(S, k_p2x_classes, dim3(1), dim3(SW_BLOCK), 0, st, S->p2ws.p, M, T, wmap, hdr);
+               hdr, wcnt, T);
         LAUNCH(S, k_p2x_keys, dim3(nb), dim3(kTB), 0, st, S->p2ws.p, M, hdr, S->p2keys.p);
         /* the active keys only: chunks past A exit, the merge ranks against ⌈A / 1024⌉ chunks */
         const int nch = (int)((M + kSortChunk - 1) / kSortChunk);
@@ -3364,8 +3477,7 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     LAUNCH(S, k_setup, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, S->jc.p, S->in_w, S->in_d, S->in_F, S->in_E,
            S->in_R, S->delta);
     SH_TRY(coll_dev_reduce(S, R0, 4, 1));
-    LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv);
-    LAUNCH(S, k_fast_lvl_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R0, sbL, C, pr->regularizer);
+    LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv, fc, sbL, C, pr->regularizer);
     FAST_TRACE("setup");
     /* the level search M_lo: ≤ 8 rounds over ≤ 64 bits (closed rounds are empty) */
     unsigned long long *srl = nullptr, *spf = nullptr;
@@ -3409,9 +3521,14 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     FAST_TRACE("between");
     /* the share placement (P1's and, in density order, P2's), then the
      * exchange step and the final evaluation on it (sw_shard_solve) */
-    SH_TRY(op_pack_share(S, SW_A_NB, SW_Y_CUR, SW_A_PL));
-    SH_TRY(eval_enqueue(S, SW_EV_PACKED, SW_A_PL, &v, nullptr));
-    LAUNCH(S, k_fast_packed, dim3(1), dim3(64), 0, st, fc, v, W, LW);
+    long long* Rd = nullptr; /* the stranded rounds, summed by the loop kernel (else PACKED below) */
+    SH_TRY(pack_share_any(S, SW_A_NB, SW_Y_CUR, SW_A_PL, &Rd));
+    if (Rd) {
+        SH_TRY(coll_dev_reduce(S, Rd, 1, 0));
+    } else {
+        SH_TRY(eval_enqueue(S, SW_EV_PACKED, SW_A_PL, &v, nullptr));
+        LAUNCH(S, k_fast_packed, dim3(1), dim3(64), 0, st, fc, v, W, LW);
+    }
     FAST_TRACE("pack");
     long long* R5 = nullptr;
     SH_TRY(p2x_enqueue(S, SW_Y_CUR, SW_A_PL, &R5, false));
@@ -3421,7 +3538,8 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     const unsigned long long seq = ++S->pub_seq;
     LAUNCH(S, k_fast_final, dim3(1), dim3(64), 0, st, (const FastCtl*)fc, (const long long*)R4,
            (const long long*)R5, v, (const unsigned long long*)srl, (const unsigned long long*)spf, W, LW,
-           reinterpret_cast<FastOut*>(S->pub_dev), S->pub_flag_dev, seq, (const int*)S->xerr);
+           reinterpret_cast<FastOut*>(S->pub_dev), S->pub_flag_dev, seq, (const int*)S->xerr,
+           (const long long*)Rd);
     FAST_TRACE("final");
 #undef FAST_TRACE
     /* one wait for the whole solve */
