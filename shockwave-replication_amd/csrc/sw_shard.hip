@@ -1550,9 +1550,9 @@ __global__ __launch_bounds__(kTB) void k_p2x_cnt(const p2x_ent* all, int64_t M, 
 }
 
 /* …and the width classes (ascending) with their sizes and offsets in hdr,
- * by the last workgroup to finish (what k_p2x_classes computed from wmap
- * and a pass over the entries, here from the workgroups' width counts
- * wcnt[w]: the same integers, one launch fewer) */
+ * computed by the last workgroup to finish from the width bitmap wmap and
+ * the workgroups' width counts wcnt[w] (no separate launch, no second pass
+ * over the entries) */
 __global__ __launch_bounds__(kTB) void k_p2x_compact(const p2x_ent* all, int64_t M, const int32_t* bcnt,
                                                      unsigned char* ws, uint32_t* wmap, int32_t* hdr,
                                                      int32_t* wcnt, int T) {
@@ -1632,53 +1632,6 @@ __global__ __launch_bounds__(kTB) void k_p2x_compact(const p2x_ent* all, int64_t
         b += ((m + 63) / 64) * T; /* word offsets, as sw_p2x_block's boff */
     }
     hdr[SW_P2X_HDR_OFF + SW_P2X_KMAX] = o;
-}
-
-/* one workgroup: the width classes (ascending) and their sizes, hdr */
-__global__ __launch_bounds__(SW_BLOCK) void k_p2x_classes(const unsigned char* ws, int64_t M, int T,
-                                                          const uint32_t* wmap, int32_t* hdr) {
-    __shared__ int32_t cls[SW_P2X_KMAX], cnt[SW_P2X_KMAX];
-    __shared__ int32_t Ks;
-    const int tid = threadIdx.x;
-    const int32_t* cw = reinterpret_cast<const int32_t*>(ws + (size_t)M * 16);
-    const int A = hdr[SW_P2X_HDR_A];
-    if (tid < SW_P2X_KMAX) cnt[tid] = 0;
-    if (tid == 0) {
-        int K = 0;
-        for (int i = 0; i < 8; ++i) K += __builtin_popcount(wmap[i]);
-        if (K > SW_P2X_KMAX) {
-            K = -1;
-        } else {
-            K = 0;
-            for (int i = 0; i < 8; ++i)
-                for (uint32_t b = wmap[i]; b; b &= b - 1) cls[K++] = 32 * i + __builtin_ctz(b);
-        }
-        Ks = K;
-    }
-    __syncthreads();
-    const int K = Ks;
-    if (K > 0)
-        for (int i = tid; i < A; i += SW_BLOCK) {
-            int k = 0;
-            while (k < K - 1 && cls[k] != cw[i]) ++k;
-            atomicAdd(&cnt[k], 1);
-        }
-    __syncthreads();
-    if (tid == 0) {
-        hdr[SW_P2X_HDR_K] = K;
-        int o = 0, b = 0;
-        for (int k = 0; k < SW_P2X_KMAX; ++k) {
-            const int m = (K >= 0 && k < K) ? cnt[k] : 0;
-            hdr[SW_P2X_HDR_WC + k] = (K >= 0 && k < K) ? cls[k] : 0;
-            hdr[SW_P2X_HDR_M + k] = m;
-            hdr[SW_P2X_HDR_OFF + k] = o;
-            hdr[SW_P2X_HDR_NW + k] = (m + 63) / 64;
-            hdr[SW_P2X_HDR_BOFF + k] = b;
-            o += m;
-            b += ((m + 63) / 64) * T; /* word offsets, as sw_p2x_block's boff */
-        }
-        hdr[SW_P2X_HDR_OFF + SW_P2X_KMAX] = o;
-    }
 }
 
 /* the rank-sort keys (class asc, sw_p2x_ckey(c) desc, job asc), as
