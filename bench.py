@@ -767,7 +767,23 @@ def c4_leg(args, world, rank, local, dist, transport="rccl"):
                    "jobs": a.N, "rounds": a.T, "ranks": world},
         "collective_steps": r["iters"],
         "matches_twin_digest": ok,
+        "transport_note": c4_transport_note(transport, world),
     }
+
+
+def c4_transport_note(transport, world):
+    """Which C4 transport this line executes for the first time (VERDICT r5
+    item 5): the builder's box has one GPU, and this image's RCCL refuses two
+    ranks on one device (profiles/r8_rccl_two_ranks_one_gpu.json), so the RCCL
+    path above world 1 and the peer transport across devices are run only by
+    the driver's multi-GPU node."""
+    if world == 1:
+        return "world 1: every collective is the identity (no RCCL call); tested on the builder's GPU"
+    if transport == "rccl":
+        return ("RCCL above world 1: not executed before this run (RCCL refuses two ranks on one device, "
+                "so no one-GPU test can run it); checked here against the committed digest")
+    return ("peer transport across devices over xGMI: not executed before this run (tested only between "
+            "ranks sharing one GPU); checked here against the committed digest")
 
 
 

@@ -140,22 +140,62 @@ static int e_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
     return E->comm->allreduce_sum_i64(E->comm->ctx, out, 2);
 }
 
-static int e_count_gt(void* ctx, const uint32_t* rho, int32_t K, int64_t* out) {
+static int e_count_gt(void* ctx, const uint32_t* rho, int32_t K, uint64_t lo, int64_t* out) {
     eng_t* E = (eng_t*)ctx;
     for (int32_t k = 0; k < K; ++k) {
         out[k] = 0;
         for (int32_t i = 0; i < E->NL; ++i) out[k] += (int64_t)E->jc[i].w * cnt(E, i, rho[k], 0);
     }
-    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K);
+    out[K] = 0; /* keys ≥ lo (lo < 2^32: a price bracket's end) */
+    for (int32_t i = 0; i < E->NL; ++i) out[K] += (int64_t)E->jc[i].w * cnt(E, i, (uint32_t)lo, 1);
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K + 1);
 }
 
-static int e_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
+static int e_feasible(void* ctx, const double* M, int32_t K, uint64_t lo, int64_t* out) {
     eng_t* E = (eng_t*)ctx;
     for (int32_t k = 0; k < K; ++k) {
         out[k] = 0;
         for (int32_t i = 0; i < E->NL; ++i) out[k] += (int64_t)E->jc[i].w * lforce(E, i, M[k]);
     }
-    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K);
+    out[K] = 0; /* levels whose bits are ≥ lo */
+    for (int32_t i = 0; i < E->NL; ++i)
+        for (int32_t n = 0; n < E->Tj[i]; ++n) out[K] += sw_bits(sw_g(&E->jc[i], n)) >= lo ? E->jc[i].w : 0;
+    return E->comm->allreduce_sum_i64(E->comm->ctx, out, K + 1);
+}
+
+/* the items of a search bracket [lo, hi] (sw_shard_ops.gather): this rank's
+ * (v, w) pairs, all-gathered in blocks of 1 + 2·SW_GATHER_CAP words */
+static int e_gather(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, uint64_t* v, int64_t* w, int32_t* n) {
+    eng_t* E = (eng_t*)ctx;
+    const int64_t bw = 1 + 2 * (int64_t)SW_GATHER_CAP;
+    int64_t* mine = (int64_t*)calloc((size_t)bw, sizeof(int64_t));
+    int64_t* all = (int64_t*)calloc((size_t)bw * (size_t)E->world, sizeof(int64_t));
+    if (!mine || !all) { free(mine); free(all); return -1; }
+    int64_t m = 0;
+    for (int32_t i = 0; i < E->NL; ++i)
+        for (int32_t t = kind ? 0 : E->l[i]; t < E->Tj[i]; ++t) {
+            const uint64_t b = kind ? sw_bits(sw_g(&E->jc[i], t)) : (uint64_t)sw_fbits_of(KEY(E, i, t));
+            if (b < lo || b > hi) continue;
+            if (m < SW_GATHER_CAP) {
+                mine[1 + 2 * m] = (int64_t)b;
+                mine[2 + 2 * m] = E->jc[i].w;
+            }
+            ++m;
+        }
+    mine[0] = m;
+    int rc = E->comm->allgather(E->comm->ctx, mine, all, bw * (int64_t)sizeof(int64_t));
+    int32_t k = 0;
+    for (int32_t r = 0; !rc && r < E->world; ++r) {
+        const int64_t* b = all + (size_t)r * bw;
+        if (b[0] > SW_GATHER_CAP || k + b[0] > SW_GATHER_CAP) { rc = -3; break; }
+        for (int64_t e = 0; e < b[0]; ++e, ++k) {
+            v[k] = (uint64_t)b[1 + 2 * e];
+            w[k] = b[2 + 2 * e];
+        }
+    }
+    *n = k;
+    free(mine); free(all);
+    return rc;
 }
 
 static int e_between(void* ctx, double a, double b, int64_t* out) {
@@ -716,6 +756,7 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.force = e_force;
     ops.count_gt = e_count_gt;
     ops.feasible = e_feasible;
+    ops.gather = e_gather;
     ops.between = e_between;
     ops.take_all = e_take_all;
     ops.take = e_take;

@@ -148,6 +148,7 @@ struct FastCtl {
 
 struct Thresholds {
     uint64_t v[SW_SHARD_K]; /* u32 key bits or fp64 bits, ascending */
+    uint64_t lo;            /* the bracket's lower end (bin 0 counts the items ≥ it) */
     int32_t K;
 };
 
@@ -306,9 +307,11 @@ __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf,
 
 /* K probes at once: item (job, n) adds w to bin #{m : thr_m < v(n)} (v =
  * the key, or g for the level probes); the count for probe m is the suffix
- * Σ_{b > m} bin[b].  Thread per item: the whole grid is busy. */
+ * Σ_{b > m} bin[b].  Bin 0 holds only the items at or above the bracket's
+ * lower end lob, so Σ_b bin[b] is that end's count (sw_shard_ops.count_gt's
+ * out[K]).  Thread per item: the whole grid is busy. */
 template <bool LEVEL>
-__device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* thr, int K,
+__device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* thr, int K, uint64_t lob,
                                            int32_t* bins) {
     /* grid-stride over the items (NL·T < 2^31): a bounded grid keeps the
      * block → global flush at ≤ kProbeBlocks·K atomics per probe */
@@ -320,11 +323,13 @@ __device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* th
         const int tj = w <= S.G ? S.T : 0;
         bool live;
         int lo = 0, hi = K;
+        uint64_t vb = 0;
         if (LEVEL) {
             live = n < tj;
             if (live) {
                 const sw_jobc c = S.jc[i];
                 const double v = sw_g(&c, n);
+                vb = sw_bits(v);
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
                     if (sw_from_bits(thr[mid]) < v) lo = mid + 1; else hi = mid;
@@ -334,6 +339,7 @@ __device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* th
             live = n >= S.l[i] && n < tj;
             if (live) {
                 const uint32_t b = sw_fbits_of(S.keys[(size_t)i * S.T + n]);
+                vb = b;
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
                     if ((uint32_t)thr[mid] < b) lo = mid + 1; else hi = mid;
@@ -341,12 +347,12 @@ __device__ __forceinline__ void probe_body(const ShardDev& S, const uint64_t* th
             }
         }
         if (live && lo == K) wtop += w;
-        else if (live && lo > 0) atomicAdd(&bins[lo], w);
+        else if (live && (lo > 0 || vb >= lob)) atomicAdd(&bins[lo], w);
     }
     wtop = wave_sum_i32(wtop);
     if (lane_id() == 0 && wtop != 0) atomicAdd(&bins[K], wtop);
     __syncthreads();
-    if (threadIdx.x <= K && threadIdx.x > 0 && bins[threadIdx.x] != 0)
+    if (threadIdx.x <= K && bins[threadIdx.x] != 0)
         atomicAdd((unsigned long long*)(S.red + threadIdx.x), (unsigned long long)bins[threadIdx.x]);
 }
 
@@ -358,15 +364,26 @@ __global__ __launch_bounds__(kTB) void k_probe(ShardDev S, Thresholds th) {
     if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
     if (threadIdx.x < th.K) thr[threadIdx.x] = th.v[threadIdx.x];
     __syncthreads();
-    probe_body<LEVEL>(S, thr, th.K, bins);
+    probe_body<LEVEL>(S, thr, th.K, th.lo, bins);
 }
 
 /* ---- device-chained K-ary search (op_search) ---------------------------------
  * The controller's swc_search loop (sw_shard_ctl.h) with its state in device
- * memory: sr[0] = lo, sr[1] = hi, sr[2] = budget (i64), sr[3] = rounds taken.
- * Each round is k_probe_dev → (RCCL all-reduce of the bins) → k_search_update
- * on the stream, with no host round trip; a round whose bracket is already
- * closed does nothing, so the host enqueues the worst-case round count. */
+ * memory: sr[0] = lo, sr[1] = hi, sr[2] = budget (i64), sr[3] = rounds taken,
+ * sr[4] = clo = Σ w·#{v ≥ lo}, sr[5] = chi = Σ w·#{v > hi} (−1: unknown),
+ * kSt words per state.  Each round is k_probe_dev → (collectives) → the step
+ * applied in the next round's kernel (or k_search_update after the last),
+ * with no host round trip.  A round's kind follows from its state
+ * (sw_search_mode): probe K thresholds into bins, or gather the bracket's
+ * items into the rank's list (SW_GATHER_CAP pairs), whose step resolves the
+ * answer; a closed bracket does nothing, so the host enqueues a bound on the
+ * rounds. */
+constexpr int kSt = 8;                            /* words of a search state */
+constexpr int kGl = 2 * (SW_GATHER_CAP + 1);      /* words of a rank's item list: count, pad, (v, w) pairs */
+/* rounds fast_solve enqueues per search: C4's level search closes in two (a
+ * probe, a gather), its price search in three (two probes, a gather); a
+ * search still open after them sends the solve to the host path */
+constexpr int kFastRounds = 3;
 struct SearchPts {
     int32_t K;
     uint64_t a, b, d;
@@ -384,18 +401,23 @@ __device__ __forceinline__ uint64_t search_pt(uint64_t lo, const SearchPts& q, i
     const uint64_t m = (uint64_t)(i + 1);
     return lo + q.a * m + (q.b * m) / q.d;
 }
-
-__global__ void k_search_init(unsigned long long* sr, unsigned long long lo, unsigned long long hi,
-                              long long bud) {
-    if (threadIdx.x == 0) { sr[0] = lo; sr[1] = hi; sr[2] = (unsigned long long)bud; sr[3] = 0; }
+__device__ __forceinline__ int search_mode(const unsigned long long* x) {
+    return sw_search_mode(x[0], x[1], (int64_t)x[4], (int64_t)x[5]);
 }
 
-/* One swc_search step on a search state x = (lo, hi, budget, rounds) from
- * the all-reduced bins of the round that probed it: counts cnt[i] =
- * Σ_{b > i} bins[b]; the first i with cnt ≤ budget closes the bracket.  One
- * wave: lane i loads bins[i + 1], a shuffle suffix scan forms cnt[i], a
- * ballot finds the first i.  Returns the new state in lane 0's out (a
- * closed bracket is left as it is). */
+__global__ void k_search_init(unsigned long long* sr, unsigned long long lo, unsigned long long hi,
+                              long long bud, long long chi) {
+    if (threadIdx.x == 0) {
+        sr[0] = lo; sr[1] = hi; sr[2] = (unsigned long long)bud; sr[3] = 0;
+        sr[4] = ~0ull; sr[5] = (unsigned long long)chi; sr[6] = 0; sr[7] = 0;
+    }
+}
+
+/* One probe step of swc_search on a state x from the all-reduced bins of the
+ * round that probed it: counts cnt[i] = Σ_{b > i} bins[b]; the first i with
+ * cnt ≤ budget closes the bracket, whose ends keep their counts.  One wave:
+ * lane i loads bins[i + 1], a shuffle suffix scan forms cnt[i], a ballot
+ * finds the first i.  Returns the new state in lane 0's out. */
 __device__ __forceinline__ void search_step_wave(const unsigned long long* x, const long long* bins,
                                                  unsigned long long* out) {
     constexpr int PL = (SW_SHARD_K + 63) / 64; /* thresholds per lane: i = PL·lane + j */
@@ -404,7 +426,7 @@ __device__ __forceinline__ void search_step_wave(const unsigned long long* x, co
     const SearchPts q = search_pts(lo, hi);
     const int lane = lane_id();
     if (q.K == 0) {
-        if (lane < 4) out[lane] = x[lane];
+        if (lane < kSt) out[lane] = x[lane];
         return;
     }
     /* cnt[i] = Σ_{b > i} bins[b]: each lane's suffix over its PL bins, then
@@ -431,6 +453,16 @@ __device__ __forceinline__ void search_step_wave(const unsigned long long* x, co
     const uint64_t ok = __ballot(fj < PL);
     const int fl = ok ? __builtin_ctzll(ok) : 0;
     const int f = ok ? PL * fl + __shfl(fj, fl, 64) : q.K;
+    /* the counts at the new ends: cnt[f] (f < K) and cnt[f − 1] (f > 0) */
+    auto cnt_at = [&](int i) -> int64_t {
+        const int jj = i % PL;
+        int64_t v = after;
+#pragma unroll
+        for (int j = 0; j < PL; ++j) v += (j == jj) ? c[j] : 0;
+        return __shfl(v, i / PL, 64);
+    };
+    const int64_t chi_n = f < q.K ? cnt_at(f) : (int64_t)x[5];
+    const int64_t clo_n = f > 0 ? cnt_at(f - 1) : cnt_at(0) + (int64_t)bins[0]; /* lo stays: bin 0 + cnt[0] */
     if (lane == 0) {
         uint64_t nlo = lo, nhi = hi;
         if (f < q.K) {
@@ -443,51 +475,178 @@ __device__ __forceinline__ void search_step_wave(const unsigned long long* x, co
         out[1] = nhi;
         out[2] = x[2];
         out[3] = x[3] + 1;
+        out[4] = (unsigned long long)clo_n;
+        out[5] = (unsigned long long)chi_n;
+        out[6] = 0;
+        out[7] = 0;
     }
 }
 
-/* Round r of the chained search: first the step of round r − 1 (its
- * all-reduced bins prev, its state xin) — every block computes it, block 0
- * stores the result in xout — then the K probes of the new bracket into
- * S.red.  Fusing the step into the next probe saves a kernel launch per
- * round; round 0 passes prev = nullptr and probes xin as it is. */
-template <bool LEVEL>
-__global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned long long* xin,
-                                                   unsigned long long* xout, const long long* prev) {
-    __shared__ int32_t bins[SW_SHARD_K + 1];
-    __shared__ uint64_t thr[SW_SHARD_K];
-    __shared__ unsigned long long xs[4];
-    if (prev == nullptr) {
-        if (threadIdx.x < 4) xs[threadIdx.x] = xin[threadIdx.x];
-    } else if (threadIdx.x < 64) {
-        search_step_wave(xin, prev, xs);
+/* The gather step of a state x (mode 2): the items of every rank's list
+ * (lists: W blocks of kGl words, rank order) resolve the answer as
+ * sw_search_resolve does — each item's sum over all items, then a minimum —
+ * by the whole block; the closed state into out (block-shared, kSt words).
+ * sm: ≥ 2·SW_GATHER_CAP + 2 words of shared scratch. */
+__device__ void search_resolve_block(const unsigned long long* x, const unsigned long long* lists, int W,
+                                     unsigned long long* out, unsigned long long* sm) {
+    unsigned long long* rv = sm;
+    long long* rw = reinterpret_cast<long long*>(sm + SW_GATHER_CAP);
+    __shared__ int rn;
+    __shared__ unsigned long long rbest;
+    __shared__ long long rslo;
+    const uint64_t lo = x[0], hi = x[1];
+    const long long bud = (long long)x[2], chi = (long long)x[5];
+    if (threadIdx.x == 0) { rn = 0; rbest = hi; rslo = 0; }
+    __syncthreads();
+    int base = 0;
+    for (int r = 0; r < W; ++r) { /* the lists' counts are uniform loads */
+        const unsigned long long* L = lists + (size_t)r * kGl;
+        int c = (int)L[0];
+        c = c < SW_GATHER_CAP - base ? c : SW_GATHER_CAP - base; /* ≤ the cap by the mode's rule */
+        for (int e = threadIdx.x; e < c; e += blockDim.x) {
+            rv[base + e] = L[2 + 2 * e];
+            rw[base + e] = (long long)L[3 + 2 * e];
+        }
+        base += c;
     }
     __syncthreads();
-    if (prev != nullptr && blockIdx.x == 0 && threadIdx.x < 4) xout[threadIdx.x] = xs[threadIdx.x];
+    const int n = base;
+    unsigned long long best = hi;
+    long long slo = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long vi = rv[i];
+        long long si = chi;
+        for (int k = 0; k < n; ++k) si += rv[k] > vi ? rw[k] : 0;
+        if (si <= bud && vi < best) best = vi;
+        slo += vi > lo ? rw[i] : 0;
+    }
+    best = wave_min_u64(best);
+    slo = wave_sum(slo);
+    if (lane_id() == 0) {
+        atomicMin(&rbest, best);
+        if (slo) atomicAdd((unsigned long long*)&rslo, (unsigned long long)slo);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = rbest;
+        if (chi + rslo <= bud) b = lo; /* lo ≤ every item */
+        out[0] = b;
+        out[1] = b;
+        out[2] = x[2];
+        out[3] = x[3] + 1;
+        out[4] = ~0ull;
+        out[5] = ~0ull;
+        out[6] = 0;
+        out[7] = 0;
+    }
+    __syncthreads();
+}
+
+/* The step of the round that ran on state x (its bins / its gathered lists)
+ * into out (block-shared), by the whole block. */
+__device__ __forceinline__ void search_step_block(const unsigned long long* x, const long long* bins,
+                                                  const unsigned long long* lists, int W, unsigned long long* out,
+                                                  unsigned long long* sm) {
+    const int m = search_mode(x);
+    if (m == 2) {
+        search_resolve_block(x, lists, W, out, sm);
+        return;
+    }
+    if (threadIdx.x < 64) {
+        if (m == 1) search_step_wave(x, bins, out);
+        else if (threadIdx.x < kSt) out[threadIdx.x] = x[threadIdx.x];
+    }
+    __syncthreads();
+}
+
+/* Items of the bracket [lo, hi] into this rank's list gl (count at gl[0];
+ * pairs beyond the cap are counted, not stored). */
+template <bool LEVEL>
+__device__ __forceinline__ void gather_body(const ShardDev& S, uint64_t lo, uint64_t hi, unsigned long long* gl) {
+    const int items = S.NL * S.T;
+    for (int e = (int)blockIdx.x * kTB + (int)threadIdx.x; e < items; e += (int)gridDim.x * kTB) {
+        const int i = e / S.T, n = e - i * S.T;
+        const int32_t w = S.jc[i].w;
+        const int tj = w <= S.G ? S.T : 0;
+        uint64_t v = 0;
+        bool in = false;
+        if (LEVEL) {
+            if (n < tj) {
+                const sw_jobc c = S.jc[i];
+                v = sw_bits(sw_g(&c, n));
+                in = v >= lo && v <= hi;
+            }
+        } else if (n >= S.l[i] && n < tj) {
+            v = sw_fbits_of(S.keys[(size_t)i * S.T + n]);
+            in = v >= lo && v <= hi;
+        }
+        if (in) {
+            const unsigned long long k = atomicAdd(gl, 1ull);
+            if (k < (unsigned long long)SW_GATHER_CAP) {
+                gl[2 + 2 * k] = v;
+                gl[3 + 2 * k] = (unsigned long long)(long long)w;
+            }
+        }
+    }
+}
+
+/* Round r of the chained search: first the step of round r − 1 (its state
+ * xin, its all-reduced bins prev or its gathered lists gprev) — every block
+ * computes it, block 0 stores the result in xout — then this round on the
+ * new state: K probes into S.red, or the bracket's items into gl.  Fusing
+ * the step into the next round saves a kernel launch per round; round 0
+ * passes prev = nullptr and runs on xin as it is. */
+template <bool LEVEL>
+__global__ __launch_bounds__(kTB) void k_probe_dev(ShardDev S, const unsigned long long* xin,
+                                                   unsigned long long* xout, const long long* prev,
+                                                   unsigned long long* gl, const unsigned long long* gprev, int W) {
+    __shared__ int32_t bins[SW_SHARD_K + 1];
+    __shared__ unsigned long long sm[2 * SW_GATHER_CAP]; /* the resolve's items, then the thresholds */
+    __shared__ unsigned long long xs[kSt];
+    if (prev == nullptr) {
+        if (threadIdx.x < kSt) xs[threadIdx.x] = xin[threadIdx.x];
+        __syncthreads();
+    } else {
+        search_step_block(xin, prev, gprev, W, xs, sm);
+    }
+    if (prev != nullptr && blockIdx.x == 0 && threadIdx.x < kSt) xout[threadIdx.x] = xs[threadIdx.x];
+    const int mode = search_mode(xs);
+    if (mode == 0) return; /* bracket closed: uniform over the grid */
     const uint64_t lo = xs[0], hi = xs[1];
+    if (mode == 2) {
+        gather_body<LEVEL>(S, lo, hi, gl);
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) gl[0] = 0; /* a later gather round appends from 0 */
     const SearchPts q = search_pts(lo, hi);
-    if (q.K == 0) return; /* bracket closed: uniform over the grid */
+    uint64_t* thr = reinterpret_cast<uint64_t*>(sm);
     if (threadIdx.x <= SW_SHARD_K) bins[threadIdx.x] = 0;
     if ((int)threadIdx.x < q.K) {
         const uint64_t v = search_pt(lo, q, (int)threadIdx.x);
         thr[threadIdx.x] = LEVEL ? v : (uint64_t)(uint32_t)v; /* price bits are u32 */
     }
     __syncthreads();
-    probe_body<LEVEL>(S, thr, q.K, bins);
+    probe_body<LEVEL>(S, thr, q.K, lo, bins);
 }
 
-/* the last round's step, in place (one wave) */
-__global__ __launch_bounds__(64) void k_search_update(unsigned long long* sr, const long long* bins,
-                                                     ShardDev S) {
-    __shared__ unsigned long long xs[4];
-    search_step_wave(sr, bins, xs);
-    __syncthreads();
-    if (threadIdx.x < 4) sr[threadIdx.x] = xs[threadIdx.x];
-    if (S.pub.dst) { /* one wave: the state to the host (fused publish) */
+/* the last round's step, in place (one block) */
+__global__ __launch_bounds__(kTB) void k_search_update(unsigned long long* sr, const long long* bins,
+                                                      const unsigned long long* lists, int W, ShardDev S) {
+    __shared__ unsigned long long sm[2 * SW_GATHER_CAP];
+    __shared__ unsigned long long xs[kSt];
+    search_step_block(sr, bins, lists, W, xs, sm);
+    if (threadIdx.x < kSt) sr[threadIdx.x] = xs[threadIdx.x];
+    if (S.pub.dst) { /* the state to the host (fused publish) */
         __threadfence();
         __syncthreads();
         pub_store(S);
     }
+}
+
+/* the items of [lo, hi] into gl alone (op_gather) */
+template <bool LEVEL>
+__global__ __launch_bounds__(kTB) void k_gather(ShardDev S, uint64_t lo, uint64_t hi, unsigned long long* gl) {
+    gather_body<LEVEL>(S, lo, hi, gl);
 }
 
 /* c (fast_solve): the interval (M_lo, M_lo + wmax] of FastCtl, nothing to
@@ -826,6 +985,10 @@ __device__ void fast_lvl_init(FastCtl* c, const long long* R0, unsigned long lon
     sr[1] = (unsigned long long)R0[3];
     sr[2] = (unsigned long long)C;
     sr[3] = 0;
+    sr[4] = ~0ull; /* clo unknown; chi = 0: no item lies above top */
+    sr[5] = 0;
+    sr[6] = 0;
+    sr[7] = 0;
 }
 
 /* after the forcing step at M_lo (swc_select): budget, every item fits or
@@ -845,6 +1008,10 @@ __global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigne
     sp[1] = all ? 0ull : (unsigned long long)SW_KEY_INF_BITS;
     sp[2] = (unsigned long long)bud;
     sp[3] = 0;
+    sp[4] = ~0ull; /* clo unknown; chi = 0: no key lies above SW_KEY_INF_BITS */
+    sp[5] = 0;
+    sp[6] = 0;
+    sp[7] = 0;
 }
 
 /* after the SELECT and UMAX evaluations: U, max g, the Lagrangian bound, the
@@ -906,7 +1073,8 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
     blocks_gm_isum(fin, blk, LW, W, gm, any);
     FastOut o;
     o.escape = c->escape || (c->did_between && R4[0] != 0) /* the branch and bound: host path */
-               || (Rd && Rd[0] != 0);                        /* stranded rounds: the share repair */
+               || (Rd && Rd[0] != 0)                         /* stranded rounds: the share repair */
+               || srl[0] < srl[1] || (!c->all && sp[0] < sp[1]); /* a search needed more rounds */
     o.utility = U;
     o.p2 = P2;
     o.makespan = gm;
@@ -2133,7 +2301,8 @@ struct sw_shard_state {
     DevBuf<unsigned char> p2ws; /* P2 exchange arrays (SW_P2X_ARR_BYTES per gathered entry), prepared set-up */
     DevBuf<sw_pack_ent> p2keys; /* the exchange's rank-sort keys (k_p2x_pre0) */
     DevBuf<unsigned char> rrin, rrrow, rrws; /* re-optimisation: gathered entries, workspace */
-    DevBuf<unsigned long long> srch; /* device-chained search states (k_search_*): level [0, 8), price [8, 16) */
+    DevBuf<unsigned long long> srch; /* device-chained search states (k_search_*): level [0, 2·kSt), price after */
+    DevBuf<unsigned long long> glist, glall; /* the searches' item lists (level, price; kGl words each), all-gathered */
     DevBuf<FastCtl> fctl;            /* fast_solve's device-side controller state */
     DevBuf<key2> skeys;   /* chunk-sorted placement keys */
     DevBuf<int32_t> sidx; /* their entries */
@@ -2444,9 +2613,10 @@ int op_force(void* ctx, double M, int32_t is_inf, int64_t out[2]) {
 }
 
 template <bool LEVEL>
-int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
+int probe(sw_shard_state* S, const uint64_t* v, int32_t K, uint64_t lo, int64_t* out) {
     Thresholds th;
     th.K = K;
+    th.lo = lo;
     for (int i = 0; i < K; ++i) th.v[i] = v[i];
     SH_TRY(zero_red(S, K + 1));
     /* the price probe is bound by its block → global flush (K atomics per
@@ -2458,73 +2628,86 @@ int probe(sw_shard_state* S, const uint64_t* v, int32_t K, int64_t* out) {
     SH_TRY(coll_reduce(S, S->dv.red, K + 1, 0, bins));
     int64_t suf = 0;
     for (int i = K - 1; i >= 0; --i) { suf += bins[i + 1]; out[i] = suf; }
+    out[K] = suf + bins[0]; /* the items ≥ lo */
     return SW_OK;
 }
 
-int op_count_gt(void* ctx, const uint32_t* rho, int32_t K, int64_t* out) {
+int op_count_gt(void* ctx, const uint32_t* rho, int32_t K, uint64_t lo, int64_t* out) {
     uint64_t v[SW_SHARD_K];
     for (int i = 0; i < K; ++i) v[i] = rho[i];
-    return probe<false>((sw_shard_state*)ctx, v, K, out);
+    return probe<false>((sw_shard_state*)ctx, v, K, lo, out);
 }
 
-int op_feasible(void* ctx, const double* M, int32_t K, int64_t* out) {
+int op_feasible(void* ctx, const double* M, int32_t K, uint64_t lo, int64_t* out) {
     uint64_t v[SW_SHARD_K];
     for (int i = 0; i < K; ++i) v[i] = sw_bits(M[i]);
-    return probe<true>((sw_shard_state*)ctx, v, K, out);
+    return probe<true>((sw_shard_state*)ctx, v, K, lo, out);
 }
 
-/* swc_search with every round on the stream: probe → (all-reduce) → update,
- * the worst-case number of rounds enqueued (closed rounds are no-ops), one
- * read-back at the end.  RCCL or a single rank only: host collectives need
- * the host between rounds and use the controller's loop. */
-/* The rounds of a device-chained K-ary search on the state at sb[0..3] (set
- * in stream order before): nr rounds probe → (collective) → the step applied
- * in the next round's probe, then the last step in place.  *fin = the final
- * state (lo = the answer, [3] = the rounds taken).  Searches whose bracket
- * closes early leave their last rounds empty. */
-int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* sb,
+/* The rounds of a device-chained search on the state at sb[0..kSt) (set in
+ * stream order before), its item list gl (kGl words): nr rounds, each a
+ * probe or a gather (by its state) → the collectives (above world 1: the
+ * bins' all-reduce, and from round 1 on, when a round may be a gather, the
+ * lists' all-gather) → the step applied in the next round, then the last
+ * step in place.  *fin = the final state (lo = the answer, [3] = the rounds
+ * taken).  Searches whose bracket closes early leave their last rounds empty. */
+int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* sb, unsigned long long* gl,
                    unsigned long long** fin, bool arm = false) {
     hipStream_t st = S->h->stream;
+    const int W = S->world;
     /* round r reads round r − 1's slice: keep the nr slices inside one pass of
      * the ring (a wrap clears the whole ring) */
     if (S->ring_pos + nr > kRing) S->ring_pos = kRing;
     const unsigned pb = nblk((int64_t)S->NL * S->T);
     const long long* prev = nullptr;
+    const unsigned long long* gview = gl; /* world 1: the rank's own list is every list */
     for (int r = 0; r < nr; ++r) {
         SH_TRY(zero_red(S, SW_SHARD_K + 1));
-        const unsigned long long* xin = sb + 4 * ((r + 1) & 1); /* X_{r−1} (X_0 for r = 0) */
-        unsigned long long* xout = sb + 4 * (r & 1);
+        const unsigned long long* xin = sb + kSt * ((r + 1) & 1); /* X_{r−1} (X_0 for r = 0) */
+        unsigned long long* xout = sb + kSt * (r & 1);
         if (r == 0) xin = sb;
         if (kind == 0)
             LAUNCH(S, k_probe_dev<false>, dim3((unsigned)probe_blocks(pb)),
-                   dim3(kTB), 0, st, S->dv, xin, xout, prev);
+                   dim3(kTB), 0, st, S->dv, xin, xout, prev, gl, gview, W);
         else
-            LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev);
-        if (S->peer)
-            SH_TRY(peer_xchg(S, S->dv.red, (size_t)(SW_SHARD_K + 1) * 8, 0, SW_SHARD_K + 1, S->dv.red));
-        else if (S->comm && S->world > 1)
-            SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
-                                     S->comm, st));
+            LAUNCH(S, k_probe_dev<true>, dim3(pb), dim3(kTB), 0, st, S->dv, xin, xout, prev, gl, gview, W);
+        if (W > 1) {
+            if (S->peer)
+                SH_TRY(peer_xchg(S, S->dv.red, (size_t)(SW_SHARD_K + 1) * 8, 0, SW_SHARD_K + 1, S->dv.red));
+            else if (S->comm)
+                SH_NCCL(S, ncclAllReduce(S->dv.red, S->dv.red, (size_t)SW_SHARD_K + 1, ncclInt64, ncclSum,
+                                         S->comm, st));
+            if (r > 0) { /* round 0 probes: no bracket's ends are known before it */
+                if (S->peer) {
+                    SH_TRY(peer_xchg(S, gl, (size_t)kGl * 8, 3, 0, nullptr));
+                    gview = (const unsigned long long*)peer_gathered(S);
+                } else if (S->comm) {
+                    SH_NCCL(S, ncclAllGather(gl, S->glall.p, (size_t)kGl * 8, ncclUint8, S->comm, st));
+                    gview = S->glall.p;
+                }
+            }
+        }
         prev = S->dv.red;
     }
-    unsigned long long* sr = sb + 4 * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
+    unsigned long long* sr = sb + kSt * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
     if (arm) SH_TRY(arm_pub(S, sr, 32)); /* world 1: the update publishes the state itself */
-    LAUNCH(S, k_search_update, dim3(1), dim3(64), 0, st, sr, prev, S->dv);
+    LAUNCH(S, k_search_update, dim3(1), dim3(kTB), 0, st, sr, prev, gview, W, S->dv);
     disarm_pub(S);
     *fin = sr;
     return SW_OK;
 }
 
-/* swc_search with every round on the stream: probe → (all-reduce) → update,
- * the worst-case number of rounds enqueued (closed rounds are no-ops), one
- * read-back at the end.  RCCL or a single rank only: host collectives need
- * the host between rounds and use the controller's loop. */
-int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, uint64_t* out,
+/* swc_search with every round on the stream (enqueue_search): the bound on
+ * the rounds enqueued (closed rounds are no-ops), one read-back at the end.
+ * RCCL, the peer transport or a single rank: host collectives need the host
+ * between rounds and use the controller's loop. */
+int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, int64_t chi, uint64_t* out,
               int32_t* rounds) {
     auto* S = (sw_shard_state*)ctx;
     hipStream_t st = S->h->stream;
-    /* each round leaves a span ≤ ⌊span / 64⌋, so the rounds are at most the
-     * base-64 digits of the initial span */
+    /* a probe round leaves a span ≤ ⌊span / (K + 1)⌋ and a gather round
+     * closes the bracket, so the rounds are at most the base-(K + 1) digits
+     * of the initial span */
     int nr = 0;
     for (uint64_t sp = lo < hi ? hi - lo : 0; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nr;
     *rounds = 0;
@@ -2532,13 +2715,41 @@ int op_search(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, int64_t bud, ui
     if (nr == 0) return SW_OK;
     unsigned long long* sb = S->srch.p;
     LAUNCH(S, k_search_init, dim3(1), dim3(64), 0, st, sb, (unsigned long long)lo,
-           (unsigned long long)hi, (long long)bud);
+           (unsigned long long)hi, (long long)bud, (long long)chi);
     unsigned long long* sr = nullptr;
-    SH_TRY(enqueue_search(S, kind, nr, sb, &sr, true));
+    SH_TRY(enqueue_search(S, kind, nr, sb, S->glist.p, &sr, true));
     unsigned long long v[4];
     SH_TRY(publish(S, sr, sizeof(v), v));
     *out = v[0];
     *rounds = (int32_t)v[3];
+    return SW_OK;
+}
+
+/* the items of a search bracket (sw_shard_ops.gather; the host-driven
+ * controller on host collectives): this rank's list, all-gathered */
+int op_gather(void* ctx, int32_t kind, uint64_t lo, uint64_t hi, uint64_t* v, int64_t* w, int32_t* n) {
+    auto* S = (sw_shard_state*)ctx;
+    hipStream_t st = S->h->stream;
+    unsigned long long* gl = S->glist.p;
+    SH_HIP(S, hipMemsetAsync(gl, 0, 16, st));
+    const unsigned pb = nblk((int64_t)S->NL * S->T);
+    if (kind == 0)
+        LAUNCH(S, k_gather<false>, dim3((unsigned)probe_blocks(pb)), dim3(kTB), 0, st, S->dv, lo, hi, gl);
+    else
+        LAUNCH(S, k_gather<true>, dim3(pb), dim3(kTB), 0, st, S->dv, lo, hi, gl);
+    std::vector<unsigned long long> all((size_t)kGl * S->world);
+    SH_TRY(coll_gather(S, gl, S->glall.p, (size_t)kGl * 8, all.data()));
+    int32_t k = 0;
+    for (int32_t r = 0; r < S->world; ++r) {
+        const unsigned long long* L = all.data() + (size_t)r * kGl;
+        if (L[0] > (unsigned long long)(SW_GATHER_CAP - k))
+            return S->h->err = "search gather: more items than SW_GATHER_CAP", SW_ERR_CAPACITY;
+        for (unsigned long long e = 0; e < L[0]; ++e, ++k) {
+            v[k] = L[2 + 2 * e];
+            w[k] = (int64_t)L[3 + 2 * e];
+        }
+    }
+    *n = k;
     return SW_OK;
 }
 
@@ -3052,7 +3263,8 @@ int prepare(sw_shard_state* S, const sw_problem* pr, int64_t off, int64_t N, boo
                S->planned.reserve(NL) || S->red.reserve((size_t)kRed * kRing) ||
                S->xrecv.reserve((xbytes / 8 + 1) * S->world) || S->pall.reserve(M) ||
                S->porder.reserve(M) || 
-               S->srch.reserve(16) || S->fctl.reserve(1) || S->scapsd.reserve((size_t)SW_VSHARES * 64 + 64) ||
+               S->srch.reserve(4 * kSt) || S->glist.reserve(2 * (size_t)kGl) ||
+               S->glall.reserve((size_t)kGl * S->world) || S->fctl.reserve(1) || S->scapsd.reserve((size_t)SW_VSHARES * 64 + 64) ||
                S->skeys.reserve(Mpad) || S->sidx.reserve(Mpad);
     for (int a = 0; a < SW_A_COUNT; ++a) bad = bad || S->arr[a].reserve(NL);
     for (int a = 0; a < SW_Y_COUNT; ++a) bad = bad || S->y[a].reserve(NL);
@@ -3138,7 +3350,7 @@ void sw_shard_release(sw_handle* h) {
     if (S->pub_flag) (void)hipHostFree(S->pub_flag);
     S->pub = nullptr; S->pub_flag = nullptr; S->pub_words = 0;
     S->p2keys.release();
-    S->srch.release(); S->skeys.release(); S->sidx.release(); S->scapsd.release(); S->fctl.release();
+    S->srch.release(); S->glist.release(); S->glall.release(); S->skeys.release(); S->sidx.release(); S->scapsd.release(); S->fctl.release();
     for (int a = 0; a < SW_A_COUNT; ++a) S->arr[a].release();
     for (int a = 0; a < SW_Y_COUNT; ++a) S->y[a].release();
     delete S;
@@ -3211,7 +3423,7 @@ static long long peer_slot_bytes(int64_t jobs, int32_t W) {
     const int64_t q = std::max<int64_t>(1, (jobs + SW_DET_LANES - 1) / SW_DET_LANES);
     const int64_t LW = SW_DET_LANES / W, P = LW * q;
     long long b = std::max<long long>({(long long)P * (long long)sizeof(sw_pack_ent), (3 * LW + 2) * 8,
-                                       P * 4, (long long)kRed * 8});
+                                       P * 4, (long long)kRed * 8, (long long)kGl * 8});
     return (b + 255) / 256 * 256;
 }
 
@@ -3421,8 +3633,10 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     const int W = S->world, LW = (int)S->LW;
     const long long C = (long long)pr->num_gpus * pr->future_rounds;
     FastCtl* fc = S->fctl.p;
-    unsigned long long* sbL = S->srch.p;     /* the level search's states */
-    unsigned long long* sbP = S->srch.p + 8; /* the price search's */
+    unsigned long long* sbL = S->srch.p;           /* the level search's states */
+    unsigned long long* sbP = S->srch.p + 2 * kSt; /* the price search's */
+    unsigned long long* glL = S->glist.p;          /* their item lists */
+    unsigned long long* glP = S->glist.p + kGl;
     disarm_pub(S);
     /* setup (op_setup): constants, key rows, the maxima */
     SH_TRY(zero_red(S, 4));
@@ -3432,11 +3646,10 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     SH_TRY(coll_dev_reduce(S, R0, 4, 1));
     LAUNCH(S, k_keys, dim3(nblk((int64_t)S->NL * 64)), dim3(kTB), 0, st, S->dv, fc, sbL, C, pr->regularizer);
     FAST_TRACE("setup");
-    /* the level search M_lo: ≤ 8 rounds over ≤ 64 bits (closed rounds are empty) */
+    /* the level search M_lo: kFastRounds rounds (a probe, then typically the
+     * gather of a small bracket; a search that needs more leaves the path) */
     unsigned long long *srl = nullptr, *spf = nullptr;
-    int nrl = 0; /* ≤ 64 bits of a level's fp64 pattern: the rounds for the widest span */
-    for (uint64_t sp = ~0ull; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nrl;
-    SH_TRY(enqueue_search(S, 1, nrl, sbL, &srl));
+    SH_TRY(enqueue_search(S, 1, kFastRounds, sbL, glL, &srl));
     FAST_TRACE("level search");
     /* SELECT(M_lo) (swc_select): force, the price search, take, assign */
     SH_TRY(zero_red(S, 2));
@@ -3445,9 +3658,7 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     SH_TRY(coll_dev_reduce(S, R1, 2, 0));
     LAUNCH(S, k_fast_price_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R1, (const unsigned long long*)srl,
            sbP);
-    int nrp = 0;
-    for (uint64_t sp = SW_KEY_INF_BITS; sp > 0; sp /= (uint64_t)(SW_SHARD_K + 1)) ++nrp; /* op_search's count */
-    SH_TRY(enqueue_search(S, 0, nrp, sbP, &spf));
+    SH_TRY(enqueue_search(S, 0, kFastRounds, sbP, glP, &spf));
     FAST_TRACE("price search");
     SH_TRY(zero_red(S, 2));
     long long* R2 = S->dv.red;
@@ -3601,6 +3812,7 @@ int slow_solve(sw_shard_state* S, const sw_problem* local, int64_t total_jobs, s
     ops.force = op_force;
     ops.count_gt = op_count_gt;
     ops.feasible = op_feasible;
+    ops.gather = op_gather;
     ops.between = op_between;
     ops.take_all = op_take_all;
     ops.take = op_take;
