@@ -146,6 +146,19 @@ struct FastCtl {
     double k, A, M_lo, U, Mact, ubound, Umax, bmax;
 };
 
+/* The last step of a device-chained search, applied by the kernel that
+ * consumes its answer (fast_solve) instead of a k_search_update launch:
+ * every block steps X_{nr−1} = x (its bins / gathered lists), block 0 stores
+ * X_nr at xo.  x = nullptr: no search to finish. */
+struct SearchTail {
+    const unsigned long long* x;
+    unsigned long long* xo;
+    const long long* bins;
+    const unsigned long long* lists;
+    int W;
+};
+__device__ uint64_t search_tail(const SearchTail& t);
+
 struct Thresholds {
     uint64_t v[SW_SHARD_K]; /* u32 key bits or fp64 bits, ascending */
     uint64_t lo;            /* the bracket's lower end (bin 0 counts the items ≥ it) */
@@ -288,8 +301,9 @@ __global__ __launch_bounds__(kTB) void k_keys(ShardDev S, FastCtl* fc = nullptr,
 
 /* Mdev (fast_solve): M = the level search's answer, its state's lo bits */
 __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf,
-                                               const unsigned long long* Mdev = nullptr) {
-    if (Mdev) M = sw_from_bits(Mdev[0]);
+                                               const unsigned long long* Mdev = nullptr, SearchTail st = {}) {
+    if (st.x) M = sw_from_bits(search_tail(st));
+    else if (Mdev) M = sw_from_bits(Mdev[0]);
     const int i = blockIdx.x * kTB + threadIdx.x;
     long long wf = 0, wall = 0;
     if (i < S.NL) {
@@ -643,6 +657,14 @@ __global__ __launch_bounds__(kTB) void k_search_update(unsigned long long* sr, c
     }
 }
 
+__device__ uint64_t search_tail(const SearchTail& t) {
+    __shared__ unsigned long long sm[2 * SW_GATHER_CAP];
+    __shared__ unsigned long long xs[kSt];
+    search_step_block(t.x, t.bins, t.lists, t.W, xs, sm);
+    if (blockIdx.x == 0 && threadIdx.x < kSt) t.xo[threadIdx.x] = xs[threadIdx.x];
+    return xs[0];
+}
+
 /* the items of [lo, hi] into gl alone (op_gather) */
 template <bool LEVEL>
 __global__ __launch_bounds__(kTB) void k_gather(ShardDev S, uint64_t lo, uint64_t hi, unsigned long long* gl) {
@@ -681,9 +703,10 @@ __global__ __launch_bounds__(kTB) void k_take_all(ShardDev S) {
 /* rdev / fc (fast_solve): ρ = the price search's answer; when every item
  * fits (fc->all) the step is k_take_all's (n := T_j, taken := T_j − l) */
 __global__ __launch_bounds__(kTB) void k_take(ShardDev S, uint32_t rho, const unsigned long long* rdev = nullptr,
-                                              const FastCtl* fc = nullptr) {
+                                              const FastCtl* fc = nullptr, SearchTail st = {}) {
     const int i = blockIdx.x * kTB + threadIdx.x;
-    if (rdev) rho = (uint32_t)rdev[0];
+    if (st.x) rho = (uint32_t)search_tail(st);
+    else if (rdev) rho = (uint32_t)rdev[0];
     const bool all = fc && fc->all;
     long long wt = 0, tie = 0;
     if (i < S.NL) {
@@ -2652,7 +2675,7 @@ int op_feasible(void* ctx, const double* M, int32_t K, uint64_t lo, int64_t* out
  * step in place.  *fin = the final state (lo = the answer, [3] = the rounds
  * taken).  Searches whose bracket closes early leave their last rounds empty. */
 int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* sb, unsigned long long* gl,
-                   unsigned long long** fin, bool arm = false) {
+                   unsigned long long** fin, bool arm = false, SearchTail* tail = nullptr) {
     hipStream_t st = S->h->stream;
     const int W = S->world;
     /* round r reads round r − 1's slice: keep the nr slices inside one pass of
@@ -2690,6 +2713,15 @@ int enqueue_search(sw_shard_state* S, int32_t kind, int nr, unsigned long long* 
         prev = S->dv.red;
     }
     unsigned long long* sr = sb + kSt * ((nr - 1) & 1); /* X_{nr−1}, stepped in place */
+    if (tail) { /* the consumer steps it: X_nr into the other half (X_{nr−2}'s, read by now) */
+        tail->x = sr;
+        tail->xo = sb + kSt * (nr & 1);
+        tail->bins = prev;
+        tail->lists = gview;
+        tail->W = W;
+        *fin = tail->xo;
+        return SW_OK;
+    }
     if (arm) SH_TRY(arm_pub(S, sr, 32)); /* world 1: the update publishes the state itself */
     LAUNCH(S, k_search_update, dim3(1), dim3(kTB), 0, st, sr, prev, gview, W, S->dv);
     disarm_pub(S);
@@ -3649,21 +3681,22 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     /* the level search M_lo: kFastRounds rounds (a probe, then typically the
      * gather of a small bracket; a search that needs more leaves the path) */
     unsigned long long *srl = nullptr, *spf = nullptr;
-    SH_TRY(enqueue_search(S, 1, kFastRounds, sbL, glL, &srl));
+    SearchTail tl{}, tp{}; /* their last steps, taken by k_force and k_take */
+    SH_TRY(enqueue_search(S, 1, kFastRounds, sbL, glL, &srl, false, &tl));
     FAST_TRACE("level search");
     /* SELECT(M_lo) (swc_select): force, the price search, take, assign */
     SH_TRY(zero_red(S, 2));
     long long* R1 = S->dv.red;
-    LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl);
+    LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl, tl);
     SH_TRY(coll_dev_reduce(S, R1, 2, 0));
     LAUNCH(S, k_fast_price_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R1, (const unsigned long long*)srl,
            sbP);
-    SH_TRY(enqueue_search(S, 0, kFastRounds, sbP, glP, &spf));
+    SH_TRY(enqueue_search(S, 0, kFastRounds, sbP, glP, &spf, false, &tp));
     FAST_TRACE("price search");
     SH_TRY(zero_red(S, 2));
     long long* R2 = S->dv.red;
     LAUNCH(S, k_take, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0u, (const unsigned long long*)spf,
-           (const FastCtl*)fc);
+           (const FastCtl*)fc, tp);
     const void* gv = R2;
     if (W > 1) SH_TRY(coll_gather(S, R2, S->xrecv.p, 16, nullptr, &gv));
     SH_TRY(zero_red(S, 1));
