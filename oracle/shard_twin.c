@@ -789,3 +789,9 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
 int shard_share_caps(const int64_t* loads, int32_t W, int32_t rank, int32_t T, int64_t G, int32_t* caps) {
     return sw_share_caps(loads, W, rank, T, G, caps);
 }
+
+/* sw_search_resolve (sw_shard_ctl.h) for tests/test_shard.py's property test. */
+uint64_t shard_search_resolve(uint64_t lo, uint64_t hi, int64_t chi, int64_t bud, const uint64_t* v,
+                              const int64_t* w, int32_t n) {
+    return sw_search_resolve(lo, hi, chi, bud, v, w, n);
+}

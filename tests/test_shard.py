@@ -400,3 +400,33 @@ def test_large_instance_same_at_every_world(shard_lib, twin):
     r16 = run_threads(shard_lib, a, 16)
     check_plan_valid(a, r16)
     assert_share_contract(r16, twin.solve(a), "W=16 large")
+
+
+def test_search_resolve_matches_brute_force(shard_lib):
+    """The gathered step of the sharded searches (sw_search_resolve,
+    DESIGN.md §7.2): the smallest x in [lo, hi) with chi + Σ_{v_i > x} w_i ≤
+    bud, else hi — against a scan over every x of small brackets, with ties,
+    items at both ends and budgets on either side of every partial sum."""
+    fn = shard_lib.shard_search_resolve
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64,
+                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+    rng = np.random.default_rng(7)
+    for _ in range(400):
+        lo = int(rng.integers(0, 1 << 40))
+        span = int(rng.integers(1, 40))
+        hi = lo + span
+        n = int(rng.integers(0, 12))
+        v = np.sort(rng.integers(lo, hi + 1, size=n)).astype(np.uint64)
+        w = rng.integers(1, 6, size=n).astype(np.int64)
+        chi = int(rng.integers(0, 4))
+        tot = chi + int(w.sum())
+        for bud in range(max(0, chi - 1), tot + 2):
+            want = hi
+            for x in range(lo, hi):
+                if chi + int(w[v > x].sum()) <= bud:
+                    want = x
+                    break
+            got = fn(lo, hi, chi, bud, v.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                     w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+            assert got == want, (lo, hi, chi, bud, v.tolist(), w.tolist(), got, want)
