@@ -652,6 +652,73 @@ static int fill_stranded(twin_t* P, int32_t* n, uint8_t* y) {
     return added;
 }
 
+/* The plan's exact objective (the emit's deterministic sum) and makespan. */
+static double plan_objective(const twin_t* P, const int32_t* n, double* tmp) {
+    double M = 0.0;
+    for (int32_t j = 0; j < P->N; ++j) {
+        tmp[j] = fval(P, j, n[j]);
+        M = sw_max(M, sw_g(&P->jc[j], n[j]));
+    }
+    return sw_detsum(tmp, P->N) - P->k * M;
+}
+
+/* Raises (sw_arith.h SW_RAISE_ITERS) on the plan n / y;
+ * returns the number kept. */
+static int raise_counts(twin_t* P, const sw_problem* pr, int32_t* n, uint8_t* y) {
+    const int32_t N = P->N, T = P->T;
+    const size_t NN = N > 0 ? (size_t)N : 1;
+    int32_t* nt = (int32_t*)malloc(sizeof(int32_t) * NN);
+    int32_t* pt = (int32_t*)malloc(sizeof(int32_t) * NN);
+    uint8_t* yt = (uint8_t*)malloc(NN * (size_t)T);
+    uint64_t* key = (uint64_t*)malloc(sizeof(uint64_t) * NN);
+    double* tmp = (double*)malloc(sizeof(double) * NN);
+    const int64_t C0 = (int64_t)P->G * T;
+    int kept = 0;
+    for (int it = 0; it < SW_RAISE_ITERS; ++it) {
+        const double J = plan_objective(P, n, tmp);
+        /* M, the first job attaining it, and the largest g of the others */
+        double M = -1.0, M2 = 0.0;
+        int32_t i1 = -1;
+        for (int32_t j = 0; j < N; ++j) {
+            const double g = sw_g(&P->jc[j], n[j]);
+            if (g > M) { if (i1 >= 0) M2 = sw_max(M2, M); M = g; i1 = j; }
+            else M2 = sw_max(M2, g);
+        }
+        if (M < 0.0) M = 0.0;
+        int64_t load = 0;
+        for (int32_t j = 0; j < N; ++j) {
+            load += (int64_t)P->jc[j].w * n[j];
+            key[j] = 0;
+            if (n[j] >= P->Tj[j]) continue;
+            const double Mo = j == i1 ? M2 : M;
+            key[j] = sw_fill_key(sw_raise_gain(fval(P, j, n[j]), fval(P, j, n[j] + 1),
+                                               sw_g(&P->jc[j], n[j] + 1), Mo, M, P->k), j, 0);
+        }
+        P->passes++;
+        int took = 0;
+        for (int tr = 0; tr < SW_RAISE_TRIES && !took; ++tr) {
+            uint64_t best = 0;
+            for (int32_t j = 0; j < N; ++j) best = key[j] > best ? key[j] : best;
+            if (best == 0) break;
+            const int32_t b = (int32_t)sw_fill_job(best);
+            key[b] = 0;
+            if (load + P->jc[b].w > C0) continue;
+            memcpy(nt, n, sizeof(int32_t) * NN);
+            nt[b] += 1;
+            if (!pattern_pack(P, pr, nt, yt, pt)) continue;
+            if (plan_objective(P, pt, tmp) > J) {
+                memcpy(n, pt, sizeof(int32_t) * NN);
+                memcpy(y, yt, NN * (size_t)T);
+                took = 1;
+            }
+        }
+        if (!took) break;
+        ++kept;
+    }
+    free(nt); free(pt); free(yt); free(key); free(tmp);
+    return kept;
+}
+
 /* ---- per-round exact re-optimisation (sw_reround.h: the specification the
  * GPU block function sw_reround_dev.h follows step for step) ---- */
 typedef struct {
@@ -991,6 +1058,12 @@ int twin_plan_solve(const sw_problem* pr, sw_result* res) {
     /* ... and re-optimise it round by round (sw_reround.h) */
     if ((status & SW_STATUS_P1_REPACKED) &&
         twin_reround_arrays(N, T, P.G, P.k, P.nb, P.beta, P.ell, P.jc, nbest, ybest, &P.passes) > 0) {
+        dens_best = 0;
+        rep_best = 0;
+        dskip_best = 0;
+    }
+    /* ... and try raises (sw_arith.h: SW_RAISE_ITERS) */
+    if ((status & SW_STATUS_P1_REPACKED) && raise_counts(&P, pr, nbest, ybest) > 0) {
         dens_best = 0;
         rep_best = 0;
         dskip_best = 0;

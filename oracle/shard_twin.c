@@ -54,6 +54,10 @@ typedef struct {
 
 #define KEY(E, i, n) ((E)->key[(size_t)(i) * (E)->T + (n)])
 
+static int e_raise_stats(void* ctx, double M, int64_t out[3]);
+static int e_raise_best(void* ctx, double M, int64_t i1, double M2, const int64_t* tried, int32_t ntried,
+                        uint64_t* best);
+
 static double fv(const eng_t* E, int32_t i, int32_t n) {
     return sw_f(&E->jc[i], n, E->nb, E->beta, E->ell, E->slope);
 }
@@ -776,6 +780,8 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     ops.search = NULL; /* the controller's own K-ary loop */
     ops.pack_share = e_pack_share;
     ops.share_repair = e_share_repair;
+    ops.raise_stats = e_raise_stats;
+    ops.raise_best = e_raise_best;
     int rc = sw_shard_solve(&ops, total_jobs, E.T, E.G, E.k, &res->objective, &res->utility,
                             &res->makespan, &res->p2_objective, &res->bound, &res->iters,
                             &res->status);
@@ -783,6 +789,68 @@ int shard_twin_solve(const sw_host_comm* comm, int32_t rank, int32_t world, cons
     for (int a = 0; a < SW_A_COUNT; ++a) free(E.arr[a]);
     for (int a = 0; a < SW_Y_COUNT; ++a) free(E.y[a]);
     return rc < 0 ? SW_ERR_RCCL : rc;
+}
+
+/* raises (sw_shard_ops.raise_stats / raise_best) */
+static int e_raise_stats(void* ctx, double M, int64_t out[3]) {
+    eng_t* E = (eng_t*)ctx;
+    /* this rank: the first job at M (global index, or INT64_MAX), #{g = M},
+     * max{g < M}, max g, Σ w·nfin — gathered, merged in rank order */
+    int64_t mine[5] = {INT64_MAX, 0, 0, 0, 0};
+    double mlt = 0.0, mall = 0.0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int32_t n = E->arr[SW_A_NFIN][i];
+        const double g = sw_g(&E->jc[i], n);
+        if (g == M) { if (mine[0] == INT64_MAX) mine[0] = E->off + i; mine[1] += 1; }
+        else if (g < M) mlt = sw_max(mlt, g);
+        mall = sw_max(mall, g);
+        mine[4] += (int64_t)E->jc[i].w * n;
+    }
+    mine[2] = (int64_t)sw_bits(mlt);
+    mine[3] = (int64_t)sw_bits(mall);
+    int64_t* all = (int64_t*)calloc((size_t)5 * E->world, sizeof(int64_t));
+    if (!all) return -1;
+    int rc = E->comm->allgather(E->comm->ctx, mine, all, 5 * (int64_t)sizeof(int64_t));
+    if (!rc) {
+        int32_t owner = -1;
+        out[0] = INT64_MAX;
+        out[2] = 0;
+        for (int32_t r = 0; r < E->world; ++r) {
+            const int64_t* b = all + (size_t)5 * r;
+            if (owner < 0 && b[0] != INT64_MAX) { owner = r; out[0] = b[0]; }
+            out[2] += b[4];
+        }
+        double M2 = 0.0;
+        for (int32_t r = 0; r < E->world; ++r) {
+            const int64_t* b = all + (size_t)5 * r;
+            const double v = r == owner ? (b[1] >= 2 ? M : sw_from_bits((uint64_t)b[2]))
+                                        : sw_from_bits((uint64_t)b[3]);
+            M2 = sw_max(M2, v);
+        }
+        out[1] = (int64_t)sw_bits(M2);
+    }
+    free(all);
+    return rc;
+}
+
+static int e_raise_best(void* ctx, double M, int64_t i1, double M2, const int64_t* tried, int32_t ntried,
+                        uint64_t* best) {
+    eng_t* E = (eng_t*)ctx;
+    uint64_t b = 0;
+    for (int32_t i = 0; i < E->NL; ++i) {
+        const int64_t j = E->off + i;
+        const int32_t n = E->arr[SW_A_NFIN][i];
+        if (n >= E->Tj[i]) continue;
+        int skip = 0;
+        for (int32_t q = 0; q < ntried; ++q) skip |= tried[q] == j;
+        if (skip) continue;
+        const double Mo = j == i1 ? M2 : M;
+        const uint64_t key = sw_fill_key(sw_raise_gain(fv(E, i, n), fv(E, i, n + 1), sw_g(&E->jc[i], n + 1),
+                                                       Mo, M, E->k), j, 0);
+        b = key > b ? key : b;
+    }
+    *best = b;
+    return E->comm->allreduce_max_u64(E->comm->ctx, best, 1);
 }
 
 /* sw_share_caps (sw_shard_ctl.h) for tests/test_shard.py's property test. */

@@ -163,6 +163,23 @@ SW_HD uint64_t sw_fill_key(double gain, int64_t j, int32_t t) {
 SW_HD int64_t sw_fill_job(uint64_t key) { return (int64_t)(0x3FFFFFFu - (uint32_t)((key >> 6) & 0x3FFFFFFu)); }
 SW_HD int32_t sw_fill_round(uint64_t key) { return (int32_t)(key & 63u); }
 
+/* Raises: after the fill and the per-round re-optimisation
+ * of a re-solved plan, up to SW_RAISE_ITERS times one job gets one more
+ * round and the whole plan is re-placed by the pattern search — a count
+ * vector the fill cannot reach when no round has room for the job until
+ * others move.  Candidates are the jobs with n_j < T_j, ranked by the gain of
+ * one more round, f_j(n_j + 1) − f_j(n_j) − k·(max(M_j⁻, g_j(n_j + 1)) − M),
+ * M the plan's makespan and M_j⁻ the largest g of the other jobs (sw_fill_key
+ * of the gain, round 0); the first SW_RAISE_TRIES are tried in that order,
+ * and a try is kept when the pattern search places it within G·T and its
+ * objective beats the plan's. */
+#define SW_RAISE_ITERS 4
+#define SW_RAISE_TRIES 4
+SW_HD double sw_raise_gain(double f0, double f1, double g1, double Mo, double M, double k) {
+    const double Mn = Mo > g1 ? Mo : g1;
+    return (f1 - f0) - k * (Mn - M);
+}
+
 /* Golden-section constants (fp64 literals, identical on both sides). */
 #define SW_GS_A 0.3819660112501051
 #define SW_GS_B 0.6180339887498949

@@ -2323,6 +2323,85 @@ __device__ __forceinline__ void solve_instance(const sw_batch_dev& B, unsigned c
             rep_best = false;
             dskip_best = false;
         }
+        /* ... and try raises (twin: raise_counts; sw_arith.h SW_RAISE_ITERS):
+         * one job one more round, the whole plan re-placed by the pattern
+         * search.  The try's counts go to nbest, its placement to ycur /
+         * placed (dead here); every decision is a block reduction */
+        for (int rit = 0; rit < SW_RAISE_ITERS; ++rit) {
+            double fs = 0.0, gm = 0.0;
+            int64_t ld_l = 0;
+            c.for_jobs([&](int j, int s) {
+                fs = fs + c.fval(j, s, c.nfin[j]);
+                gm = sw_max(gm, c.gval(j, s, c.nfin[j]));
+                ld_l += (int64_t)c.jc(j, s).w * c.nfin[j];
+            });
+            double U, M;
+            c.blk.detsum_max(fs, gm, U, M);
+            const double J = U - c.k * M;
+            const int64_t load = c.blk.sum(ld_l);
+            int32_t i1l = 0x7FFFFFFF; /* the first job attaining M, and the others' max */
+            c.for_jobs([&](int j, int s) {
+                if (j < i1l && c.gval(j, s, c.nfin[j]) == M) i1l = j;
+            });
+            const int32_t i1 = c.blk.min32(i1l);
+            double m2l = 0.0;
+            c.for_jobs([&](int j, int s) {
+                if (j != i1) m2l = sw_max(m2l, c.gval(j, s, c.nfin[j]));
+            });
+            const double M2 = c.blk.dmax(m2l);
+            c.passes++;
+            int32_t tried[SW_RAISE_TRIES];
+            bool took = false;
+            for (int tr = 0; tr < SW_RAISE_TRIES && !took; ++tr) {
+                uint64_t kl = 0;
+                c.for_jobs([&](int j, int s) {
+                    const int n = c.nfin[j];
+                    if (n >= c.Tj(j, s)) return;
+                    for (int q = 0; q < tr; ++q)
+                        if (tried[q] == j) return;
+                    const double Mo = j == i1 ? M2 : M;
+                    const uint64_t key = sw_fill_key(sw_raise_gain(c.fval(j, s, n), c.fval(j, s, n + 1),
+                                                                   c.gval(j, s, n + 1), Mo, M, c.k),
+                                                     j, 0);
+                    kl = key > kl ? key : kl;
+                });
+                const uint64_t best = c.blk.umax(kl);
+                if (best == 0) break; /* uniform */
+                const int b = (int)sw_fill_job(best);
+                tried[tr] = b;
+                if (load + c.w_in[b] > (int64_t)c.G * c.T) continue;
+                /* pattern_pack rewrites the rows of the jobs with rounds; the
+                 * others' rows (scratch of the re-optimisation) are cleared, as
+                 * the twin's pattern_pack clears its output */
+                c.for_jobs([&](int j, int s) {
+                    (void)s;
+                    c.nbest[j] = (uint8_t)(c.nfin[j] + (j == b ? 1 : 0));
+                    c.ycur[j] = 0;
+                    c.placed[j] = 0;
+                });
+                if (!c.pattern_pack(c.nbest, c.ycur, c.placed, pscr)) continue; /* uniform */
+                double fs2 = 0.0, gm2 = 0.0;
+                c.for_jobs([&](int j, int s) {
+                    fs2 = fs2 + c.fval(j, s, c.placed[j]);
+                    gm2 = sw_max(gm2, c.gval(j, s, c.placed[j]));
+                });
+                double U2, Mb2;
+                c.blk.detsum_max(fs2, gm2, U2, Mb2);
+                if (U2 - c.k * Mb2 > J) {
+                    c.for_jobs([&](int j, int s) {
+                        (void)s;
+                        c.nfin[j] = c.placed[j];
+                        c.ybest[j] = c.ycur[j];
+                    });
+                    took = true;
+                }
+            }
+            __syncthreads();
+            if (!took) break;
+            dens_best = false;
+            rep_best = false;
+            dskip_best = false;
+        }
     }
     /* ---- P2 (twin: the P2 block): (a) density order, (b) weight order,
      *      (c) class-wise inside the P1 profile — first that places every

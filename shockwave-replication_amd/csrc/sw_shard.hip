@@ -811,6 +811,61 @@ __global__ __launch_bounds__(kTB) void k_tail_best(ShardDev S, long long rem2) {
 
 __global__ void k_tail_apply(ShardDev S, int i) { S.arr[SW_A_N][i] += 1; }
 
+/* raises (sw_shard_ops.raise_stats): red[0] = ~ the first global job with
+ * g(nfin) = M (max of ~index; 0 if none here), red[1] = #{g = M}, red[2] =
+ * max bits of {g < M}, red[3] = max bits of g (g ≥ 0: bits order as
+ * values), red[4] = Σ w·nfin */
+__global__ __launch_bounds__(kTB) void k_raise_stats(ShardDev S, double M) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t first = 0, mlt = 0, mall = 0;
+    long long cnt = 0, load = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int n = S.arr[SW_A_NFIN][i];
+        const double g = sw_g(&c, n);
+        if (g == M) {
+            first = ~(uint64_t)(S.off + i);
+            cnt = 1;
+        } else if (g < M) {
+            mlt = sw_bits(g);
+        }
+        mall = sw_bits(g);
+        load = (long long)c.w * n;
+    }
+    red_umax(S.red + 0, first);
+    red_add(S.red + 1, cnt);
+    red_umax(S.red + 2, mlt);
+    red_umax(S.red + 3, mall);
+    red_add(S.red + 4, load);
+    pub_tail(S);
+}
+
+/* raises (sw_shard_ops.raise_best): the best untried candidate's key */
+struct RaiseTried {
+    long long j[SW_RAISE_TRIES];
+    int n;
+};
+__global__ __launch_bounds__(kTB) void k_raise_best(ShardDev S, double M, long long i1, double M2, RaiseTried rt) {
+    const int i = blockIdx.x * kTB + threadIdx.x;
+    uint64_t key = 0;
+    if (i < S.NL) {
+        const sw_jobc c = S.jc[i];
+        const int n = S.arr[SW_A_NFIN][i];
+        const long long j = S.off + i;
+        bool skip = n >= tj_of(S, c);
+        for (int q = 0; q < rt.n; ++q) skip |= rt.j[q] == j;
+        if (!skip) {
+            const double Mo = j == i1 ? M2 : M;
+            key = sw_fill_key(sw_raise_gain(sw_f(&c, n, S.nb, S.beta, S.ell, S.slope),
+                                            sw_f(&c, n + 1, S.nb, S.beta, S.ell, S.slope), sw_g(&c, n + 1), Mo, M,
+                                            S.k),
+                              j, 0);
+        }
+    }
+    red_umax(S.red, key);
+    pub_tail(S);
+}
+
 /* fill of stranded capacity (sw_shard_ops.fill_best / fill_apply) */
 struct FillLoad {
     long long v[SW_TMAX]; /* GPUs in use per round, all ranks */
@@ -2842,6 +2897,47 @@ int op_tail_apply(void* ctx, int64_t jb) {
     return SW_OK;
 }
 
+int op_raise_stats(void* ctx, double M, int64_t out[3]) {
+    auto* S = (sw_shard_state*)ctx;
+    SH_TRY(zero_red(S, 5));
+    SH_TRY(arm_pub(S, S->dv.red, 40));
+    LAUNCH(S, k_raise_stats, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, M);
+    disarm_pub(S);
+    /* per rank, gathered: the owner of the first job at M is the lowest rank
+     * holding one (ranks hold ascending job ranges) */
+    std::vector<unsigned long long> all((size_t)5 * S->world);
+    SH_TRY(coll_gather(S, S->dv.red, S->xrecv.p, 40, all.data()));
+    int owner = -1;
+    out[0] = INT64_MAX;
+    out[2] = 0;
+    for (int r = 0; r < S->world; ++r) {
+        const unsigned long long* b = all.data() + (size_t)5 * r;
+        if (owner < 0 && b[0] != 0) { owner = r; out[0] = (int64_t)~b[0]; }
+        out[2] += (int64_t)b[4];
+    }
+    double M2 = 0.0;
+    for (int r = 0; r < S->world; ++r) {
+        const unsigned long long* b = all.data() + (size_t)5 * r;
+        const double v = r == owner ? (b[1] >= 2 ? M : sw_from_bits(b[2])) : sw_from_bits(b[3]);
+        M2 = sw_max(M2, v);
+    }
+    out[1] = (int64_t)sw_bits(M2);
+    return SW_OK;
+}
+
+int op_raise_best(void* ctx, double M, int64_t i1, double M2, const int64_t* tried, int32_t ntried,
+                  uint64_t* best) {
+    auto* S = (sw_shard_state*)ctx;
+    RaiseTried rt;
+    rt.n = ntried < SW_RAISE_TRIES ? ntried : SW_RAISE_TRIES;
+    for (int q = 0; q < SW_RAISE_TRIES; ++q) rt.j[q] = q < rt.n ? (long long)tried[q] : -1;
+    SH_TRY(zero_red(S, 1));
+    SH_TRY(arm_pub(S, S->dv.red, 8));
+    LAUNCH(S, k_raise_best, dim3(nblk(S->NL)), dim3(kTB), 0, S->h->stream, S->dv, M, (long long)i1, M2, rt);
+    disarm_pub(S);
+    return coll_reduce(S, S->dv.red, 1, 1, best);
+}
+
 int op_fill_best(void* ctx, const int64_t* load, uint64_t* best) {
     auto* S = (sw_shard_state*)ctx;
     FillLoad L;
@@ -3865,6 +3961,8 @@ int slow_solve(sw_shard_state* S, const sw_problem* local, int64_t total_jobs, s
     ops.search = (S->host_comm && !S->peer) ? nullptr : op_search; /* host collectives need the host per round */
     ops.pack_share = op_pack_share;
     ops.share_repair = op_share_repair;
+    ops.raise_stats = op_raise_stats;
+    ops.raise_best = op_raise_best;
     static const bool trace = getenv("SW_FAST_TRACE") != nullptr;
     if (trace) fprintf(stderr, "slow_solve: start (dirty %d)\n", (int)dirty);
     int rc = sw_shard_solve(&ops, total_jobs, local->future_rounds, local->num_gpus,

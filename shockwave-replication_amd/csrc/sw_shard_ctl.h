@@ -169,6 +169,14 @@ typedef struct sw_shard_ops {
      * the pack stranded rounds of its own jobs; no collective. */
     int (*pack_share)(void* ctx, int32_t src, int32_t ydst, int32_t pdst);
     int (*share_repair)(void* ctx, int32_t src, int32_t ydst, int32_t pdst);
+    /* raises (sw_arith.h SW_RAISE_ITERS) on the plan arr[SW_A_NFIN], M its
+     * makespan: out[0] = the first job j with g_j(nfin_j) = M, out[1] = the
+     * bits of max_{j ≠ out[0]} g_j(nfin_j), out[2] = Σ w·nfin, all ranks */
+    int (*raise_stats)(void* ctx, double M, int64_t out[3]);
+    /* max over jobs with nfin_j < T_j not in tried[0..ntried) of
+     * sw_fill_key(sw_raise_gain(…), j, 0), Mo = M2 for job i1 and M else */
+    int (*raise_best)(void* ctx, double M, int64_t i1, double M2, const int64_t* tried, int32_t ntried,
+                      uint64_t* best);
 } sw_shard_ops;
 
 /* Job range of `rank` (sw_dist_shard_range in include/shockwave_amd.h). */
@@ -776,6 +784,50 @@ static inline int sw_shard_solve(const sw_shard_ops* o, int64_t N, int32_t T, in
             SWC_RUN(o->reround(o->ctx, &moves));
             c->steps++;
             if (moves > 0) {
+                dens_best = 0;
+                rep_best = 0;
+                dskip_best = 0;
+            }
+            /* ... and try raises (twin: raise_counts): one job one more round,
+             * the plan re-placed by the pattern search (on arr[SW_A_N], its rows
+             * first reset by a density pack) */
+            for (int rit = 0; rit < SW_RAISE_ITERS; ++rit) {
+                int64_t isum, rs[3];
+                SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_NFIN, c->lanesA, c->lanesB, &gm, &isum));
+                c->steps++;
+                const double J = sw_shard_tree(c->lanesA) - c->k * gm, M = gm;
+                SWC_RUN(o->raise_stats(o->ctx, M, rs));
+                c->steps++;
+                const double M2 = sw_from_bits((uint64_t)rs[1]);
+                int64_t tried[SW_RAISE_TRIES];
+                int took = 0;
+                for (int tr = 0; tr < SW_RAISE_TRIES && !took; ++tr) {
+                    uint64_t best;
+                    SWC_RUN(o->raise_best(o->ctx, M, rs[0], M2, tried, tr, &best));
+                    c->steps++;
+                    if (best == 0) break;
+                    const int64_t b = sw_fill_job(best);
+                    tried[tr] = b;
+                    int32_t wb;
+                    SWC_RUN(swc_width(c, b, &wb));
+                    if (rs[2] + wb > (int64_t)c->G * c->T) continue;
+                    SWC_RUN(o->copy(o->ctx, SW_A_N, SW_A_NFIN));
+                    SWC_RUN(o->tail_apply(o->ctx, b));
+                    SWC_RUN(o->pack(o->ctx, 4, SW_A_N, 0.0, SW_Y_CUR, SW_A_PL));
+                    c->steps++;
+                    int pok = 0;
+                    SWC_RUN(swc_pattern(c, SW_A_N, SW_Y_CUR, SW_A_PL, &pok));
+                    if (!pok) continue;
+                    int64_t dfc;
+                    SWC_RUN(o->eval(o->ctx, SW_EV_PACKED, SW_A_PL, c->lanesA, c->lanesB, &gm, &dfc));
+                    c->steps++;
+                    if (sw_shard_tree(c->lanesA) - c->k * gm > J) {
+                        SWC_RUN(o->copy(o->ctx, SW_A_NFIN, SW_A_PL));
+                        SWC_RUN(o->copy_y(o->ctx, SW_Y_BEST, SW_Y_CUR));
+                        took = 1;
+                    }
+                }
+                if (!took) break;
                 dens_best = 0;
                 rep_best = 0;
                 dskip_best = 0;
