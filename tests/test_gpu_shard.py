@@ -271,7 +271,7 @@ def test_gpu_shard_pattern_placement(world, rccl_solver, twin, shard_lib):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     import make_frag_fuzz as mk
 
-    for s in (50115, 50417, 50439, 50104):
+    for s in (50115, 50417, 50439, 50104, 50169):  # 50169: a kept raise
         a = mk.instance(s)
         r = rccl_solver.dist_solve(a, 0, a.N) if world == 1 else gpu_shard_threads(a, world)
         check_plan_valid(a, r)

@@ -294,14 +294,16 @@ def test_sharded_pattern_placement_equals_single(world, shard_lib, twin):
     """Frag-fuzz instances whose level-search counts only the round-pattern
     search places (sw_profile_search: 50115 with widths {1, 2, 4, 8} on 13
     GPUs, 50417, 50439) or that the branch and bound changes (50104, 12 width
-    classes): the controller's pattern step gathers the classes' count
-    histograms (class_caps, SW_CLASS_HIST) and runs the same search."""
+    classes), and 50169, where a raise (one more round for a width-6 job, the
+    plan re-placed; sw_arith.h SW_RAISE_ITERS) closes a 0.52 gap: the
+    controller's pattern step gathers the classes' count histograms
+    (class_caps, SW_CLASS_HIST) and runs the same search."""
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     import make_frag_fuzz as mk
 
-    for s in (50115, 50417, 50439, 50104):
+    for s in (50115, 50417, 50439, 50104, 50169):
         a = mk.instance(s)
         rs = run_threads(shard_lib, a, world)
         check_plan_valid(a, rs)
