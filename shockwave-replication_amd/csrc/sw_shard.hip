@@ -299,9 +299,17 @@ __global__ __launch_bounds__(kTB) void k_keys(ShardDev S, FastCtl* fc = nullptr,
 
 /* ---- SELECT steps ----------------------------------------------------------- */
 
-/* Mdev (fast_solve): M = the level search's answer, its state's lo bits */
+struct FastCtl;
+__device__ void fast_price_init(FastCtl* c, long long Wf, long long Wall, unsigned long long Mbits,
+                                unsigned long long* sp);
+
+/* Mdev (fast_solve): M = the level search's answer, its state's lo bits.
+ * fpi (fast_solve at world 1, where the force's sums need no collective):
+ * the last block to finish also sets up the price search (k_fast_price_init's
+ * work, one launch fewer) */
 __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf,
-                                               const unsigned long long* Mdev = nullptr, SearchTail st = {}) {
+                                               const unsigned long long* Mdev = nullptr, SearchTail st = {},
+                                               FastCtl* fpi = nullptr, unsigned long long* sp = nullptr) {
     if (st.x) M = sw_from_bits(search_tail(st));
     else if (Mdev) M = sw_from_bits(Mdev[0]);
     const int i = blockIdx.x * kTB + threadIdx.x;
@@ -316,6 +324,21 @@ __global__ __launch_bounds__(kTB) void k_force(ShardDev S, double M, int is_inf,
     }
     red_add(S.red + 0, wf);
     red_add(S.red + 1, wall);
+    if (fpi) { /* uniform: a kernel argument */
+        __shared__ int last_;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            last_ = atomicAdd((unsigned long long*)(S.red + kRedCtr), 1ull) == (unsigned long long)(gridDim.x - 1);
+        __syncthreads();
+        if (last_ && threadIdx.x == 0) {
+            __threadfence();
+            const long long Wf = __hip_atomic_load(S.red + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long Wall = __hip_atomic_load(S.red + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fast_price_init(fpi, Wf, Wall, sw_bits(M), sp);
+        }
+        return;
+    }
     pub_tail(S);
 }
 
@@ -682,6 +705,7 @@ __global__ __launch_bounds__(kTB) void k_between(ShardDev S, double a, double b,
         b = c->bmax;
         run = c->did_between != 0;
     }
+    if (c && i < S.NL) S.arr[SW_A_NB][i] = S.arr[SW_A_N][i]; /* fast_solve: swc_level_search's copy */
     if (run && i < S.NL) {
         const sw_jobc c = S.jc[i];
         const int n1 = tj_of(S, c) + 1;
@@ -1071,11 +1095,9 @@ __device__ void fast_lvl_init(FastCtl* c, const long long* R0, unsigned long lon
 
 /* after the forcing step at M_lo (swc_select): budget, every item fits or
  * the price search's bracket [0, SW_KEY_INF_BITS) */
-__global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigned long long* srl,
-                                  unsigned long long* sp) {
-    if (threadIdx.x != 0) return;
-    const long long Wf = R1[0], Wall = R1[1];
-    c->M_lo = sw_from_bits(srl[0]);
+__device__ void fast_price_init(FastCtl* c, long long Wf, long long Wall, unsigned long long Mbits,
+                                unsigned long long* sp) {
+    c->M_lo = sw_from_bits(Mbits);
     if (Wf > c->C) c->escape = 1; /* not at M_lo: a guard */
     const long long bud = c->C - Wf;
     const int all = Wall <= bud || Wf > c->C;
@@ -1090,6 +1112,10 @@ __global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigne
     sp[5] = 0;
     sp[6] = 0;
     sp[7] = 0;
+}
+__global__ void k_fast_price_init(FastCtl* c, const long long* R1, const unsigned long long* srl,
+                                  unsigned long long* sp) {
+    if (threadIdx.x == 0) fast_price_init(c, R1[0], R1[1], srl[0], sp);
 }
 
 /* after the SELECT and UMAX evaluations: U, max g, the Lagrangian bound, the
@@ -3783,10 +3809,15 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     /* SELECT(M_lo) (swc_select): force, the price search, take, assign */
     SH_TRY(zero_red(S, 2));
     long long* R1 = S->dv.red;
-    LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl, tl);
-    SH_TRY(coll_dev_reduce(S, R1, 2, 0));
-    LAUNCH(S, k_fast_price_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R1, (const unsigned long long*)srl,
-           sbP);
+    if (W == 1) { /* the force's last block sets up the price search */
+        LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl, tl,
+               fc, sbP);
+    } else {
+        LAUNCH(S, k_force, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0, (const unsigned long long*)srl, tl);
+        SH_TRY(coll_dev_reduce(S, R1, 2, 0));
+        LAUNCH(S, k_fast_price_init, dim3(1), dim3(64), 0, st, fc, (const long long*)R1,
+               (const unsigned long long*)srl, sbP);
+    }
     SH_TRY(enqueue_search(S, 0, kFastRounds, sbP, glP, &spf, false, &tp));
     FAST_TRACE("price search");
     SH_TRY(zero_red(S, 2));
@@ -3810,7 +3841,7 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     long long* R4 = S->dv.red;
     LAUNCH(S, k_between, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0.0, 0.0, (const FastCtl*)fc);
     SH_TRY(coll_dev_reduce(S, R4, 1, 0));
-    SH_TRY(op_copy(S, SW_A_NB, SW_A_N));
+    /* (k_between also copied the counts arr[SW_A_N] into arr[SW_A_NB]) */
     FAST_TRACE("between");
     /* the share placement (P1's and, in density order, P2's), then the
      * exchange step and the final evaluation on it (sw_shard_solve) */
