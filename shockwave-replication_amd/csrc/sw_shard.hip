@@ -142,7 +142,7 @@ struct ShardDev {
  * the host then solves it again with the host-driven controller. */
 struct FastCtl {
     long long C, bud, Wall, wt, rem, used;
-    int all, escape, did_between, pad;
+    int all, escape, did_between, tail_steps; /* tail_steps: the width tail's steps (k_fast_tail) */
     double k, A, M_lo, U, Mact, ubound, Umax, bmax;
 };
 
@@ -688,6 +688,55 @@ __device__ uint64_t search_tail(const SearchTail& t) {
     return xs[0];
 }
 
+/* The width tail of SELECT at world 1 (swc_select's loop: while room is
+ * left, the job whose next key is largest among those that fit — key << 32 |
+ * ~job, k_tail_best's order — takes one more round), by one workgroup over
+ * every job, before the SELECT evaluation.  fc->tail_steps = the steps the
+ * controller counts: one per tail_best, plus the widths' gather on the first
+ * round taken. */
+constexpr int kTailTB = 1024;
+__global__ __launch_bounds__(kTailTB) void k_fast_tail(ShardDev S, FastCtl* fc, const long long* R3) {
+    __shared__ unsigned long long wb[kTailTB / 64];
+    __shared__ unsigned long long bb;
+    const int tid = threadIdx.x;
+    if (fc->all || fc->escape) { /* uniform */
+        if (tid == 0) fc->tail_steps = 0;
+        return;
+    }
+    long long rem2 = fc->rem - R3[0];
+    int steps = 0, took = 0;
+    while (rem2 > 0) {
+        unsigned long long best = 0;
+        for (int i = tid; i < S.NL; i += kTailTB) {
+            const sw_jobc c = S.jc[i];
+            const int n = S.arr[SW_A_N][i];
+            if (n < tj_of(S, c) && (long long)c.w <= rem2) {
+                const unsigned long long kk = ((unsigned long long)sw_fbits_of(S.keys[(size_t)i * S.T + n]) << 32) |
+                                              (unsigned long long)(0xFFFFFFFFu - (uint32_t)(S.off + i));
+                best = kk > best ? kk : best;
+            }
+        }
+        best = wave_max(best);
+        if (lane_id() == 0) wb[wave_id()] = best;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long b = 0;
+            for (int w = 0; w < kTailTB / 64; ++w) b = wb[w] > b ? wb[w] : b;
+            bb = b;
+        }
+        __syncthreads();
+        best = bb;
+        ++steps;
+        if (best == 0) break; /* uniform */
+        const int jb = (int)((long long)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu)) - S.off);
+        if (tid == 0) S.arr[SW_A_N][jb] += 1;
+        rem2 -= S.jc[jb].w;
+        took = 1;
+        __syncthreads(); /* the count is read by every thread next step */
+    }
+    if (tid == 0) fc->tail_steps = steps + took;
+}
+
 /* the items of [lo, hi] into gl alone (op_gather) */
 template <bool LEVEL>
 __global__ __launch_bounds__(kTB) void k_gather(ShardDev S, uint64_t lo, uint64_t hi, unsigned long long* gl) {
@@ -1134,7 +1183,7 @@ __global__ __launch_bounds__(64) void k_fast_sel_ctl(FastCtl* c, const long long
     long long is;
     blocks_gm_isum(sel, blk, LW, W, gm, is);
     const int all = c->all;
-    if (!all && c->rem - R3[0] > 0) c->escape = 1; /* the width tail: host path */
+    if (W > 1 && !all && c->rem - R3[0] > 0) c->escape = 1; /* the width tail above world 1: host path */
     const double rho_d = all ? 0.0 : (double)sw_float_of((uint32_t)sp[0]);
     const long long wgt = all ? c->Wall : c->wt;
     c->U = U;
@@ -1191,7 +1240,7 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
     o.status = st;
     /* setup, level rounds, force, [price rounds, take, assign], SELECT, UMAX,
      * [between], share pack, PACKED, exchange, FINAL (swc_* step counts) */
-    o.iters = (int32_t)(1 + (long long)srl[3] + 1 + (c->all ? 0 : (long long)sp[3] + 2) + 2 +
+    o.iters = (int32_t)(1 + (long long)srl[3] + 1 + (c->all ? 0 : (long long)sp[3] + 2 + c->tail_steps) + 2 +
                         (c->did_between ? 1 : 0) + 4);
     o.xerr = xerr ? *xerr : 0;
     *hout = o;
@@ -3830,6 +3879,9 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
     long long* R3 = S->dv.red;
     LAUNCH(S, k_assign, dim3(nblk(S->NL)), dim3(kTB), 0, st, S->dv, 0ll, 0ll, fc, (const long long*)gv, W);
     SH_TRY(coll_dev_reduce(S, R3, 1, 0));
+    /* world 1: the width tail on the device (above it the tail's collectives
+     * are host steps: k_fast_sel_ctl sends the solve to the host path) */
+    if (W == 1) LAUNCH(S, k_fast_tail, dim3(1), dim3(kTailTB), 0, st, S->dv, fc, (const long long*)R3);
     FAST_TRACE("take/assign");
     /* the SELECT evaluation and swc_level_search's utility optimum in one
      * pass, then the level values in (M_lo, M_lo + wmax] (none: M_lo wins) */

@@ -90,6 +90,21 @@ def test_gpu_shard_c4_shape(rccl_solver, twin, shard_lib):
     assert_share_contract(r, twin.solve(a), "C4 vs single")
 
 
+@pytest.mark.parametrize("seed", [71, 73, 74])
+def test_gpu_shard_c4_seeds(seed, rccl_solver, shard_lib):
+    """Other C4-shaped instances (tools/c4_seeds.py): 71 ends SELECT with a
+    width tail (on the device at world 1, k_fast_tail), 73 strands rounds in a
+    share (the host path's share repair), 74 takes the common path; each the
+    CPU shard engine's result bit for bit, collective steps included."""
+    c = ss.C4
+    a = ss.synth_problem(seed, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
+    r = rccl_solver.dist_solve(a, 0, a.N)
+    check_plan_valid(a, r)
+    ref = run_threads(shard_lib, a, 1)
+    assert_same_as_single(r, ref, f"C4 seed {seed}")
+    assert r["iters"] == ref["iters"], (seed, r["iters"], ref["iters"])
+
+
 def test_gpu_shard_c4_world8(shard_lib):
     c = ss.C4
     a = ss.synth_problem(12, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
