@@ -1216,7 +1216,8 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
                                                    const long long* R5, const double* fin,
                                                    const unsigned long long* srl, const unsigned long long* sp,
                                                    int W, int LW, FastOut* hout, unsigned long long* hflag,
-                                                   unsigned long long hseq, const int* xerr, const long long* Rd) {
+                                                   unsigned long long hseq, const int* xerr, const long long* Rd,
+                                                   int extra_iters = 0, int extra_status = 0) {
     const int blk = 2 * LW + 2;
     const double U = wave_tree512(fin, blk, LW, 0);
     const double P2 = wave_tree512(fin, blk, LW, LW);
@@ -1225,15 +1226,18 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
     long long any;
     blocks_gm_isum(fin, blk, LW, W, gm, any);
     FastOut o;
-    o.escape = c->escape || (c->did_between && R4[0] != 0) /* the branch and bound: host path */
-               || (Rd && Rd[0] != 0)                         /* stranded rounds: the share repair */
-               || srl[0] < srl[1] || (!c->all && sp[0] < sp[1]); /* a search needed more rounds */
+    /* 1 = the host-driven controller solves it again; 2 = only the share
+     * placement stranded rounds: the host repairs the shares and the rest of
+     * the path runs again on this state (fast_resume) */
+    const bool other = c->escape || (c->did_between && R4 && R4[0] != 0) /* the branch and bound */
+                       || srl[0] < srl[1] || (!c->all && sp[0] < sp[1]); /* a search needed more rounds */
+    o.escape = other ? 1 : (Rd && Rd[0] != 0) ? 2 : 0;
     o.utility = U;
     o.p2 = P2;
     o.makespan = gm;
     o.objective = U - c->k * gm;
     o.bound = c->ubound - c->k * c->M_lo;
-    int32_t st = 0;
+    int32_t st = extra_status;
     if (R5[0] > 0) st |= SW_STATUS_P2_EXCHANGED;
     if (any == 0) st |= SW_STATUS_NO_PLANNED;
     if (sw_p1_uncertified(o.objective, o.bound)) st |= SW_STATUS_P1_UNCERTIFIED;
@@ -1241,7 +1245,7 @@ __global__ __launch_bounds__(64) void k_fast_final(const FastCtl* c, const long 
     /* setup, level rounds, force, [price rounds, take, assign], SELECT, UMAX,
      * [between], share pack, PACKED, exchange, FINAL (swc_* step counts) */
     o.iters = (int32_t)(1 + (long long)srl[3] + 1 + (c->all ? 0 : (long long)sp[3] + 2 + c->tail_steps) + 2 +
-                        (c->did_between ? 1 : 0) + 4);
+                        (c->did_between ? 1 : 0) + 4 + extra_iters);
     o.xerr = xerr ? *xerr : 0;
     *hout = o;
     __threadfence_system();
@@ -2084,9 +2088,12 @@ __global__ __launch_bounds__(kTB) void k_p2x_pre_w(const int32_t* hdr, const dou
  * same on every rank; writes this rank's rows of ydst and the number of
  * cycles cancelled into red[0].  pre: the prepared set-up (k_p2x_pre*; the
  * X arrays are then already compacted in ws). */
+/* skip (fast_solve): the share placement stranded rounds — leave the
+ * placement as it is for the share repair that follows on the host */
 __global__ __launch_bounds__(SW_BLOCK) void k_p2x(ShardDev S, const p2x_ent* all, int64_t M,
                                                   unsigned char* ws, uint64_t* ydst, sw_p2x_pre pre,
-                                                  int prepared) {
+                                                  int prepared, const long long* skip = nullptr) {
+    if (skip && skip[0] != 0) return; /* uniform */
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     sw_p2x_lds* L = reinterpret_cast<sw_p2x_lds*>(smem);
     unsigned char* var = smem + ((sizeof(sw_p2x_lds) + 15) & ~(size_t)15);
@@ -3325,7 +3332,8 @@ int op_class_caps(void* ctx, int32_t src, int32_t ysrc, int32_t wc, int32_t psrc
  * exchange step replicated, keep this rank's rows */
 /* the exchange step on the stream; *res = the step slot whose [0] receives
  * the cycles cancelled (the same on every rank); arm: publish it (world 1) */
-int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, bool arm) {
+int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, bool arm,
+                const long long* skip = nullptr) {
     hipStream_t st = S->h->stream;
     const int64_t M = S->P * S->world;
     p2x_ent* mine = reinterpret_cast<p2x_ent*>(S->pall.p + (size_t)S->rank * S->P);
@@ -3389,7 +3397,7 @@ int p2x_enqueue(sw_shard_state* S, int32_t ysrc, int32_t nsrc, long long** res, 
     }
     if (arm) SH_TRY(arm_pub(S, S->dv.red, 8));
     LAUNCH(S, k_p2x, dim3(1), dim3(SW_BLOCK), lds, st, S->dv, (const p2x_ent*)gv, M, S->p2ws.p,
-           S->y[ysrc].p, pre, (int)prepared);
+           S->y[ysrc].p, pre, (int)prepared, skip);
     disarm_pub(S);
     *res = S->dv.red;
     return SW_OK;
@@ -3906,39 +3914,61 @@ int fast_solve(sw_shard_state* S, const sw_problem* pr, int64_t N, sw_result* re
         LAUNCH(S, k_fast_packed, dim3(1), dim3(64), 0, st, fc, v, W, LW);
     }
     FAST_TRACE("pack");
-    long long* R5 = nullptr;
-    SH_TRY(p2x_enqueue(S, SW_Y_CUR, SW_A_PL, &R5, false));
-    FAST_TRACE("p2x");
-    SH_TRY(eval_enqueue(S, SW_EV_FINAL, SW_Y_CUR, &v, nullptr));
-    SH_TRY(publish_reserve(S, sizeof(FastOut) / 4 + 1));
-    const unsigned long long seq = ++S->pub_seq;
-    LAUNCH(S, k_fast_final, dim3(1), dim3(64), 0, st, (const FastCtl*)fc, (const long long*)R4,
-           (const long long*)R5, v, (const unsigned long long*)srl, (const unsigned long long*)spf, W, LW,
-           reinterpret_cast<FastOut*>(S->pub_dev), S->pub_flag_dev, seq, (const int*)S->xerr,
-           (const long long*)Rd);
-    FAST_TRACE("final");
-#undef FAST_TRACE
-    /* one wait for the whole solve */
-    auto t0 = std::chrono::steady_clock::now();
-    uint32_t spins = 0;
-    while (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq) {
-        __builtin_ia32_pause();
-        if (((++spins) & 0xFFFFu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
-            SH_HIP(S, hipStreamSynchronize(st));
-            if (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq)
-                return S->h->err = "fast path: the result never arrived", SW_ERR_HIP;
-            break;
+    /* the exchange step, the final evaluation and the result (twice when the
+     * share placement stranded rounds: again after the host's share repair) */
+    auto finish = [&](const long long* R4f, const long long* Rdf, int extra_iters, int extra_status,
+                      FastOut& o) -> int {
+        long long* R5 = nullptr;
+        SH_TRY(p2x_enqueue(S, SW_Y_CUR, SW_A_PL, &R5, false, Rdf));
+        FAST_TRACE("p2x");
+        SH_TRY(eval_enqueue(S, SW_EV_FINAL, SW_Y_CUR, &v, nullptr));
+        SH_TRY(publish_reserve(S, sizeof(FastOut) / 4 + 1));
+        const unsigned long long seq = ++S->pub_seq;
+        LAUNCH(S, k_fast_final, dim3(1), dim3(64), 0, st, (const FastCtl*)fc, R4f, (const long long*)R5, v,
+               (const unsigned long long*)srl, (const unsigned long long*)spf, W, LW,
+               reinterpret_cast<FastOut*>(S->pub_dev), S->pub_flag_dev, seq, (const int*)S->xerr, Rdf,
+               extra_iters, extra_status);
+        FAST_TRACE("final");
+        /* one wait for the whole solve */
+        auto t0 = std::chrono::steady_clock::now();
+        uint32_t spins = 0;
+        while (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq) {
+            __builtin_ia32_pause();
+            if (((++spins) & 0xFFFFu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+                SH_HIP(S, hipStreamSynchronize(st));
+                if (__atomic_load_n(S->pub_flag, __ATOMIC_ACQUIRE) < seq)
+                    return S->h->err = "fast path: the result never arrived", SW_ERR_HIP;
+                break;
+            }
         }
-    }
+        memcpy(&o, S->pub, sizeof(o));
+        if (trace)
+            fprintf(stderr, "fast_solve: escape %d objective %.17g iters %d status %d\n", o.escape, o.objective,
+                    o.iters, o.status);
+        if (o.xerr) {
+            S->xfailed = true; /* sticky: the ranks stopped at different exchanges */
+            return S->h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+        }
+        return SW_OK;
+    };
     FastOut o;
-    memcpy(&o, S->pub, sizeof(o));
-    if (trace)
-        fprintf(stderr, "fast_solve: escape %d objective %.17g iters %d status %d\n", o.escape, o.objective,
-                o.iters, o.status);
-    if (o.xerr) {
-        S->xfailed = true; /* sticky: the ranks stopped at different exchanges */
-        return S->h->err = "peer exchange: a rank's flag never arrived (timed out)", SW_ERR_RCCL;
+    SH_TRY(finish((const long long*)R4, (const long long*)Rd, 0, 0, o));
+    if (o.escape == 2) {
+        /* only the share placement stranded rounds (sw_shard_solve): the
+         * shares' repair (host: sw_profile_repair, then class repacks on the
+         * device), its PACKED evaluation — one more collective step — and,
+         * when it places every count, the rest of the path on this state (the
+         * exchange left the placement as it was); P2 is the repaired density
+         * placement (SW_STATUS_P2_REPAIRED) */
+        SH_TRY(op_share_repair(S, SW_A_NB, SW_Y_CUR, SW_A_PL));
+        double gmr;
+        int64_t dfc = 0;
+        std::vector<double> la((size_t)SW_DET_LANES), lb((size_t)SW_DET_LANES);
+        SH_TRY(op_eval(S, SW_EV_PACKED, SW_A_PL, la.data(), lb.data(), &gmr, &dfc));
+        if (dfc != 0) return 2; /* the gathered orders: the host-driven controller */
+        SH_TRY(finish(nullptr, nullptr, 1, SW_STATUS_P2_REPAIRED, o));
     }
+#undef FAST_TRACE
     if (o.escape) return 2;
     res->objective = o.objective;
     res->utility = o.utility;

@@ -90,12 +90,13 @@ def test_gpu_shard_c4_shape(rccl_solver, twin, shard_lib):
     assert_share_contract(r, twin.solve(a), "C4 vs single")
 
 
-@pytest.mark.parametrize("seed", [71, 73, 74])
+@pytest.mark.parametrize("seed", [71, 73, 74, 75])
 def test_gpu_shard_c4_seeds(seed, rccl_solver, shard_lib):
     """Other C4-shaped instances (tools/c4_seeds.py): 71 ends SELECT with a
-    width tail (on the device at world 1, k_fast_tail), 73 strands rounds in a
-    share (the host path's share repair), 74 takes the common path; each the
-    CPU shard engine's result bit for bit, collective steps included."""
+    width tail (on the device at world 1, k_fast_tail), 73 and 75 strand
+    rounds in a share (the host's share repair, then the rest of the device
+    path: fast_solve's resume), 74 takes the common path; each the CPU shard
+    engine's result bit for bit, collective steps included."""
     c = ss.C4
     a = ss.synth_problem(seed, c["N"], c["G"], c["T"], c["delta"], c["k"], c["lam"])
     r = rccl_solver.dist_solve(a, 0, a.N)
