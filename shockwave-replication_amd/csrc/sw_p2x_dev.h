@@ -335,9 +335,54 @@ static __device__ __forceinline__ double p2x_cost_dir(const uint64_t* Bt, const 
  * two triangles, all u < t first, so every wave but one has a single move
  * direction (one code path of p2x_cost_dir); pair i of a triangle is (a, b),
  * b < a, with a(a − 1)/2 ≤ i < a(a + 1)/2. */
-template <int NT>
-static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const uint64_t* B, const double* pc,
-                                                   double* W, int8_t* Wk, int T, double delta, bool all) {
+/* pair e of the two triangles (u < t first) */
+static __device__ __forceinline__ void p2x_pair(int e, int P, int& t, int& u) {
+    const bool lo = e < P;
+    const int i = lo ? e : e - P;
+    int a = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)i)) * 0.5f);
+    if (a * (a - 1) / 2 > i) --a;
+    if ((a + 1) * a / 2 <= i) ++a;
+    const int b = i - a * (a - 1) / 2;
+    t = lo ? a : b;
+    u = lo ? b : a;
+}
+
+/* The cheapest class's cost of the edge t → u (W, Wk entry). */
+static __device__ __forceinline__ void p2x_edge(const sw_p2x_lds* L, const uint64_t* B, const double* pc,
+                                                double* W, int8_t* Wk, int T, double delta, int K, int t,
+                                                int u) {
+    const bool lo = u < t;
+    double best = SW_P2X_NONE;
+    int bk = -1;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+        const int q = L->fq[k];
+        if (q == 0) continue;
+        const int nw = L->nw[k];
+        const uint64_t* Bk = B + L->boff[k]; /* word-major: word w of round t at w·T + t */
+        const double cost = lo ? p2x_cost_dir<true>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k])
+                               : p2x_cost_dir<false>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k]);
+        if (cost < best) {
+            best = cost;
+            bk = k;
+        }
+    }
+    W[t * T + u] = bk >= 0 ? best + delta : SW_P2X_NONE;
+    Wk[t * T + u] = (int8_t)bk;
+}
+
+/* After a cancel (all = false) only the pairs in a row or column of the
+ * touched rounds change — 2·n·(T − 1) − n·(n − 1) of the T(T − 1) for n
+ * touched rounds, ≈ 170 of 870 at T = 30 after a 3-round cycle.  Walking
+ * all pairs left most lanes idle and the busy ones with two pairs each; the
+ * touched pairs are listed first (lst, in pair order: the u < t triangle
+ * first, so the waves keep one move direction) and dealt one per thread.
+ * lst (the move records, free until the next cycle's moves) holds
+ * SW_P2X_MAX_MOVES entries; a longer list takes the pair walk. */
+template <int NT, class BLK>
+static __device__ __forceinline__ void p2x_build_w(BLK& blk, const sw_p2x_lds* L, const uint64_t* B,
+                                                   const double* pc, double* W, int8_t* Wk, int T, double delta,
+                                                   bool all, int32_t* lst) {
     const uint64_t tm = L->touched;
     const int K = L->K;
     const int P = T * (T - 1) / 2;
@@ -346,32 +391,37 @@ static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const ui
             W[t * T + t] = SW_P2X_NONE;
             Wk[t * T + t] = (int8_t)-1;
         }
-    for (int e = threadIdx.x; e < 2 * P; e += NT) {
-        const bool lo = e < P;
-        const int i = lo ? e : e - P;
-        int a = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)i)) * 0.5f);
-        if (a * (a - 1) / 2 > i) --a;
-        if ((a + 1) * a / 2 <= i) ++a;
-        const int b = i - a * (a - 1) / 2;
-        const int t = lo ? a : b, u = lo ? b : a;
-        if (!all && !(((tm >> t) | (tm >> u)) & 1ull)) continue;
-        double best = SW_P2X_NONE;
-        int bk = -1;
-#pragma unroll 1
-        for (int k = 0; k < K; ++k) {
-            const int q = L->fq[k];
-            if (q == 0) continue;
-            const int nw = L->nw[k];
-            const uint64_t* Bk = B + L->boff[k]; /* word-major: word w of round t at w·T + t */
-            const double cost = lo ? p2x_cost_dir<true>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k])
-                                   : p2x_cost_dir<false>(Bk + t, Bk + u, nw, T, q, t, u, pc + L->off[k]);
-            if (cost < best) {
-                best = cost;
-                bk = k;
+    if (!all) {
+        const int nt = __popcll(tm);
+        if (2 * nt * (T - 1) - nt * (nt - 1) <= SW_P2X_MAX_MOVES) {
+            const int c = (2 * P + NT - 1) / NT;
+            const int e0 = threadIdx.x * c, e1 = min(2 * P, e0 + c);
+            int cnt = 0;
+            for (int e = e0; e < e1; ++e) {
+                int t, u;
+                p2x_pair(e, P, t, u);
+                cnt += (((tm >> t) | (tm >> u)) & 1ull) ? 1 : 0;
             }
+            int tot;
+            int pos = blk.exscan(cnt, tot);
+            for (int e = e0; e < e1; ++e) {
+                int t, u;
+                p2x_pair(e, P, t, u);
+                if (((tm >> t) | (tm >> u)) & 1ull) lst[pos++] = (t << 6) | u;
+            }
+            __syncthreads();
+            for (int j = threadIdx.x; j < tot; j += NT) {
+                const int v = lst[j];
+                p2x_edge(L, B, pc, W, Wk, T, delta, K, v >> 6, v & 63);
+            }
+            return;
         }
-        W[t * T + u] = bk >= 0 ? best + delta : SW_P2X_NONE;
-        Wk[t * T + u] = (int8_t)bk;
+    }
+    for (int e = threadIdx.x; e < 2 * P; e += NT) {
+        int t, u;
+        p2x_pair(e, P, t, u);
+        if (!all && !(((tm >> t) | (tm >> u)) & 1ull)) continue;
+        p2x_edge(L, B, pc, W, Wk, T, delta, K, t, u);
     }
 }
 
@@ -762,7 +812,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                         Wk[e] = Wkb[e];
                     }
                 } else {
-                    p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
+                    p2x_build_w<NT>(blk, L, B, pc, W, Wk, T, delta, all, rec);
                 }
                 __syncthreads();
                 P2X_STAMP(3);
