@@ -299,6 +299,19 @@ __device__ __forceinline__ void sw_pack_rounds(BLK& blk, sw_pack_lds* L, int A, 
     __syncthreads();
 }
 
+/* The width a tier (or the fill) took, without a reduction: a position is
+ * taken when it is eligible, its eligible prefix ex is below the tier's quota
+ * and ex + w fits the round, and both tests fail for every later eligible
+ * position once they fail for one (ex grows by at least the failing width),
+ * so the taken positions are a prefix of the eligible ones.  The wave's last
+ * lane that took any then holds the end of that prefix: its eligible base
+ * plus its own take (its eligible positions before its first untaken one). */
+__device__ __forceinline__ int32_t sw_pack_took(int32_t base, int32_t took) {
+    const uint64_t mk = __ballot(took > 0);
+    if (mk == 0) return 0;
+    return __builtin_amdgcn_readlane(base + took, 63 - __builtin_clzll(mk));
+}
+
 /*
  * The same round loop run by ONE wave over E1 positions per lane
  * (position p = E1·lane + i, so a wave exclusive scan of the lane totals is
@@ -384,7 +397,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
                 took += take ? WW_(i) : 0;
                 st[i] = take ? (st[i] & 0xFFFFu) : st[i];
             }
-            took = wave_sum_i32(took);
+            took = sw_pack_took(base, took);
             cap -= took;
             red += took;
             mstart = m - 1;
@@ -407,7 +420,7 @@ __device__ __forceinline__ void sw_pack_rounds_wave(sw_pack_lds* L, int T, int G
                 took += take ? WW_(i) : 0;
                 st[i] = take ? (st[i] & 0xFFFFu) : st[i];
             }
-            cap -= wave_sum_i32(took);
+            cap -= sw_pack_took(base, took);
         }
         SWP_STAMP(3);
         while (cap > 0) {
