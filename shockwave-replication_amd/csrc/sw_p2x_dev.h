@@ -371,18 +371,31 @@ static __device__ __forceinline__ void p2x_edge(const sw_p2x_lds* L, const uint6
     Wk[t * T + u] = (int8_t)bk;
 }
 
+/* Touched pairs (a, b), a > b, a or b in S, in rows < a: all pairs of the
+ * first a rows less those with neither round in S (a ≤ 63). */
+static __device__ __forceinline__ int p2x_rows_before(uint64_t S, int a) {
+    const int m = a - __popcll(S & ((1ull << a) - 1ull));
+    return a * (a - 1) / 2 - m * (m - 1) / 2;
+}
+
 /* After a cancel (all = false) only the pairs in a row or column of the
- * touched rounds change — 2·n·(T − 1) − n·(n − 1) of the T(T − 1) for n
+ * touched rounds S change — 2·n·(T − 1) − n·(n − 1) of the T(T − 1) for n
  * touched rounds, ≈ 170 of 870 at T = 30 after a 3-round cycle.  Walking
  * all pairs left most lanes idle and the busy ones with two pairs each; the
- * touched pairs are listed first (lst, in pair order: the u < t triangle
- * first, so the waves keep one move direction) and dealt one per thread.
- * lst (the move records, free until the next cycle's moves) holds
- * SW_P2X_MAX_MOVES entries; a longer list takes the pair walk. */
-template <int NT, class BLK>
-static __device__ __forceinline__ void p2x_build_w(BLK& blk, const sw_p2x_lds* L, const uint64_t* B,
+ * touched pairs are dealt one per thread instead, in pair order (the u < t
+ * triangle first, so the waves keep one move direction).  Thread j finds
+ * its pair without a list: the touched pairs of the lower triangle are
+ * counted row by row in closed form (p2x_rows_before), so a binary search
+ * over the rows gives the row a, and the column is the r-th round of the
+ * row's touched columns (all of them when a is in S, else the rounds of S
+ * below a); the upper triangle is the transpose, in the same order.  (A
+ * block-scanned list in LDS measured the same, but its loop spilled 8 B per
+ * lane more in the fused pack kernel, and one wave listing them by ballots
+ * was slower on the C5 sweep.) */
+template <int NT>
+static __device__ __forceinline__ void p2x_build_w(const sw_p2x_lds* L, const uint64_t* B,
                                                    const double* pc, double* W, int8_t* Wk, int T, double delta,
-                                                   bool all, int32_t* lst) {
+                                                   bool all) {
     const uint64_t tm = L->touched;
     const int K = L->K;
     const int P = T * (T - 1) / 2;
@@ -392,35 +405,32 @@ static __device__ __forceinline__ void p2x_build_w(BLK& blk, const sw_p2x_lds* L
             Wk[t * T + t] = (int8_t)-1;
         }
     if (!all) {
-        const int nt = __popcll(tm);
-        if (2 * nt * (T - 1) - nt * (nt - 1) <= SW_P2X_MAX_MOVES) {
-            const int c = (2 * P + NT - 1) / NT;
-            const int e0 = threadIdx.x * c, e1 = min(2 * P, e0 + c);
-            int cnt = 0;
-            for (int e = e0; e < e1; ++e) {
-                int t, u;
-                p2x_pair(e, P, t, u);
-                cnt += (((tm >> t) | (tm >> u)) & 1ull) ? 1 : 0;
+        const uint64_t S = T < 64 ? tm & ((1ull << T) - 1ull) : tm;
+        const int nt = __popcll(S);
+        const int half = nt * (T - 1) - nt * (nt - 1) / 2;
+        for (int j = threadIdx.x; j < 2 * half; j += NT) {
+            const bool lo = j < half;
+            const int i = lo ? j : j - half;
+            int a0 = 1, a1 = T - 1;
+            while (a0 < a1) {
+                const int mid = (a0 + a1 + 1) >> 1;
+                if (p2x_rows_before(S, mid) <= i) a0 = mid;
+                else a1 = mid - 1;
             }
-            int tot;
-            int pos = blk.exscan(cnt, tot);
-            for (int e = e0; e < e1; ++e) {
-                int t, u;
-                p2x_pair(e, P, t, u);
-                if (((tm >> t) | (tm >> u)) & 1ull) lst[pos++] = (t << 6) | u;
+            const int r = i - p2x_rows_before(S, a0);
+            int b = r;
+            if (!((S >> a0) & 1ull)) {
+                uint64_t m = S & ((1ull << a0) - 1ull);
+                for (int k = 0; k < r; ++k) m &= m - 1ull;
+                b = __ffsll((long long)m) - 1;
             }
-            __syncthreads();
-            for (int j = threadIdx.x; j < tot; j += NT) {
-                const int v = lst[j];
-                p2x_edge(L, B, pc, W, Wk, T, delta, K, v >> 6, v & 63);
-            }
-            return;
+            p2x_edge(L, B, pc, W, Wk, T, delta, K, lo ? a0 : b, lo ? b : a0);
         }
+        return;
     }
     for (int e = threadIdx.x; e < 2 * P; e += NT) {
         int t, u;
         p2x_pair(e, P, t, u);
-        if (!all && !(((tm >> t) | (tm >> u)) & 1ull)) continue;
         p2x_edge(L, B, pc, W, Wk, T, delta, K, t, u);
     }
 }
@@ -812,7 +822,7 @@ __device__ __forceinline__ int sw_p2x_block(sw_blk_t<NW>& blk, sw_p2x_lds* L, un
                         Wk[e] = Wkb[e];
                     }
                 } else {
-                    p2x_build_w<NT>(blk, L, B, pc, W, Wk, T, delta, all, rec);
+                    p2x_build_w<NT>(L, B, pc, W, Wk, T, delta, all);
                 }
                 __syncthreads();
                 P2X_STAMP(3);
