@@ -221,6 +221,10 @@ void sw_destroy(sw_handle* h) {
         if (ev) (void)hipEventDestroy(ev);
     if (h->up) (void)hipStreamDestroy(h->up);
     if (h->dn) (void)hipStreamDestroy(h->dn);
+    for (hipEvent_t ev : h->ev_xs)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t x : h->xs)
+        if (x) (void)hipStreamDestroy(x);
     for (hipEvent_t ev : h->ev_pool)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : h->ev_p2x)
@@ -448,7 +452,8 @@ int h2d(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s) {
 /* The solve kernels for instances [lo, hi) of the loaded batch on s: the
  * per-instance arrays offset to lo, the per-job ones global (each
  * descriptor holds its global job and plan offsets). */
-int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed, bool want_masks) {
+int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed, bool want_masks,
+           int force_split = -1) {
     sw_batch_dev B;
     memset(&B, 0, sizeof(B));
     B.want_masks = want_masks ? 1 : 0;
@@ -500,7 +505,7 @@ int launch(sw_handle* h, int32_t lo, int32_t hi, hipStream_t s, bool timed, bool
 #ifdef SW_STAMPS
     const bool split = false; /* diagnostic builds time the phases inside the full kernel */
 #else
-    const bool split = one && B.count > split_min_count();
+    const bool split = one && (force_split >= 0 ? force_split != 0 : B.count > split_min_count());
 #endif
     B.fuse_p2x = one && (split || B.count <= fuse_max_count()); /* split: always fused */
     if (B.fuse_p2x) lds = std::max(lds, sw_p2x_kernel_lds_bytes(h->maxN, h->maxT));
@@ -653,6 +658,64 @@ int solve_pipelined(sw_handle* h, int32_t count, const sw_problem* probs, sw_res
     return rc ? SW_FALLBACK : SW_OK;
 }
 
+/* Streams for sw_batch_run (SW_RUN_STREAMS overrides).  A split batch is
+ * three launches, each waiting for its slowest instance, so a split batch
+ * that does not fill the chip many times over (the 512-instance C5 sweep:
+ * two instances per CU) ends with the slowest level search followed by the
+ * slowest pack + exchange — of different instances.  Cut into contiguous
+ * chunks on their own streams, a chunk's pack kernel starts when that
+ * chunk's level searches are done, and the batch ends with the slowest
+ * chunk's own chain.  Results are per instance, so the cut changes none. */
+constexpr int kMaxRunStreams = 4; /* GPU_MAX_HW_QUEUES is 4 on the box */
+
+int run_streams(const sw_handle* h) {
+    static const int req = [] {
+        const char* e = getenv("SW_RUN_STREAMS");
+        return e ? atoi(e) : -1;
+    }();
+#ifdef SW_STAMPS
+    return 1; /* diagnostic builds time the phases inside the full kernel */
+#endif
+    const bool one = h->maxN <= SW_LDS_JOBS && h->maxT <= 32;
+    if (!one || h->count <= split_min_count()) return 1; /* not a split batch */
+    int ns = req >= 0 ? req : (h->count <= 2048 ? 2 : 1);
+    ns = std::max(1, std::min(ns, kMaxRunStreams));
+    return std::min(ns, std::max(1, h->count / 64)); /* chunks of at least 64 */
+}
+
+int launch_streams(sw_handle* h, int ns) {
+    if (h->xs.empty()) {
+        h->xs.assign(kMaxRunStreams - 1, nullptr);
+        h->ev_xs.assign(kMaxRunStreams, nullptr);
+        for (auto& x : h->xs) SW_HIP(h, hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        for (auto& ev : h->ev_xs) SW_HIP(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    const bool timed = h->timing;
+    if (timed) {
+        if (h->ev_used == kEventPairs && collect_timing(h) != SW_OK) return SW_ERR_HIP;
+        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used], h->stream));
+    }
+    SW_HIP(h, hipEventRecord(h->ev_xs[0], h->stream)); /* fork: the upload is done */
+    for (int c = 1; c < ns; ++c) SW_HIP(h, hipStreamWaitEvent(h->xs[c - 1], h->ev_xs[0], 0));
+    int err = SW_OK;
+    for (int c = 0; c < ns && err == SW_OK; ++c) {
+        const int32_t lo = (int32_t)((int64_t)h->count * c / ns), hi = (int32_t)((int64_t)h->count * (c + 1) / ns);
+        err = launch(h, lo, hi, c == 0 ? h->stream : h->xs[c - 1], false, h->keep_masks, 1);
+    }
+    for (int c = 1; c < ns; ++c) { /* join (also after a failed launch: nothing may still run) */
+        SW_HIP(h, hipEventRecord(h->ev_xs[c], h->xs[c - 1]));
+        SW_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xs[c], 0));
+    }
+    if (err != SW_OK) return err;
+    if (timed) { /* the exchange runs inside the plan launches: an empty p2x interval */
+        SW_HIP(h, hipEventRecord(h->ev_pool[2 * h->ev_used + 1], h->stream));
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used], h->stream));
+        SW_HIP(h, hipEventRecord(h->ev_p2x[2 * h->ev_used + 1], h->stream));
+        h->ev_used++;
+    }
+    return SW_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -690,7 +753,9 @@ int sw_batch_run(sw_handle* h) {
     if (h->count <= 0) return SW_OK;
     SW_HIP(h, hipSetDevice(h->device));
     h->masks_valid = h->keep_masks;
-    return launch(h, 0, h->count, h->stream, h->timing, h->keep_masks);
+    const int ns = run_streams(h);
+    if (ns <= 1) return launch(h, 0, h->count, h->stream, h->timing, h->keep_masks);
+    return launch_streams(h, ns);
 }
 
 int sw_batch_keep_masks(sw_handle* h, int32_t keep) {

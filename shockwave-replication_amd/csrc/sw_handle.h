@@ -104,6 +104,10 @@ struct sw_handle {
      * per-chunk events, created on first use */
     hipStream_t up = nullptr, dn = nullptr;
     std::vector<hipEvent_t> ev_chunk;
+    /* sw_batch_run over several streams (run_streams in sw_api.hip): the
+     * extra streams and their fork / join events, created on first use */
+    std::vector<hipStream_t> xs;
+    std::vector<hipEvent_t> ev_xs;
     /* the batch being uploaded (described once its upload completes) */
     int32_t pend_count = 0;
     int64_t pend_jobs = 0, pend_plan = 0;
