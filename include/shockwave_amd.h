@@ -176,7 +176,12 @@ int sw_plan_solve_batch(sw_handle* h, int32_t count, const sw_problem* problems,
  * callers that keep the SoA on the GPU):
  *   sw_batch_upload   copies `count` problems into the handle's device SoA;
  *   sw_batch_run      enqueues the solve kernels on the handle's stream
- *                     (asynchronous, no host sync, graph-capturable);
+ *                     (asynchronous, no host sync, graph-capturable); a
+ *                     split batch of at most 2048 instances runs as two
+ *                     chunks on the handle's stream and one internal stream
+ *                     forked from and joined back into it by events, so the
+ *                     call stays ordered on the handle's stream
+ *                     (SW_RUN_STREAMS overrides the count, 1..4);
  *   sw_batch_download synchronises and copies plans/results back.
  */
 int sw_batch_upload(sw_handle* h, int32_t count, const sw_problem* problems);
