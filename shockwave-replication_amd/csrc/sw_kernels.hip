@@ -1855,7 +1855,7 @@ __device__ __forceinline__ void pack_tail(const sw_batch_dev& B, const uint64_t*
     const int N = I->N, T = I->T, G = I->G;
     const int64_t jo = I->job_off;
     const int q = (N + SW_BLOCK - 1) / SW_BLOCK; /* ≤ 2: N ≤ SW_LDS_JOBS */
-    const int j0 = (int)threadIdx.x * q, j1 = min(j0 + q, N);
+    const int j0 = sw_tid_opaque() * q, j1 = min(j0 + q, N);
     __syncthreads(); /* the emit's status and ym are final; the pack's reductions are read */
     int act = 0;
 #pragma unroll

@@ -24,11 +24,19 @@
  * L2-resident while the instance runs) so that the LDS holds only the step's
  * own state (~30 KB at 900 jobs × 30 rounds).
  */
-/* thread tid's jobs [j0, j1) of an N-job instance (the plan kernel's split) */
-__device__ __forceinline__ int j0r(int N) { return (int)threadIdx.x * ((N + SW_BLOCK - 1) / SW_BLOCK); }
+/* thread tid's jobs [j0, j1) of an N-job instance (the plan kernel's split).
+ * The thread index goes through an empty asm so every call recomputes the
+ * bound (one multiply) instead of the compiler keeping one copy live across
+ * the exchange step: at the pack kernel's 64-VGPR cap that copy was spilled. */
+__device__ __forceinline__ int sw_tid_opaque() {
+    int x = (int)threadIdx.x;
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int j0r(int N) { return sw_tid_opaque() * ((N + SW_BLOCK - 1) / SW_BLOCK); }
 __device__ __forceinline__ int j1r(int N) {
     const int q = (N + SW_BLOCK - 1) / SW_BLOCK;
-    return min((int)threadIdx.x * q + q, N);
+    return min(sw_tid_opaque() * q + q, N);
 }
 
 __device__ __forceinline__ void sw_p2x_instance(const sw_batch_dev& B, unsigned char* ws,
