@@ -76,9 +76,16 @@ def pmc_traffic(batch: int, jobs: int, rounds: int):
     (profiles/*_summary.json, FETCH_SIZE ×2 per the gfx950 note + WRITE_SIZE),
     when they were collected on this exact workload; else None."""
     import glob
+    import re
+
+    def tag_order(path):
+        # newest evidence set last: r<round><suffix>_summary.json by (round, suffix)
+        # (a plain name sort would put r9z after r17)
+        m = re.match(r"r(\d+)([a-z0-9]*)_summary\.json$", os.path.basename(path))
+        return (int(m.group(1)), m.group(2)) if m else (-1, os.path.basename(path))
 
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=tag_order):
         try:
             d = json.load(open(path))
         except Exception:
